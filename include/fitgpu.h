@@ -1,0 +1,169 @@
+/* fitgpu.h — C-ABI of the MI355X batched job→node placement engine (libfitgpu.so).
+ *
+ * This is the cgo seam of the new pkg/fitgpu.  The reference has no fit loop
+ * of its own (capacity is summed in pkg/slurm-virtual-kubelet/node.go:169-199 and the fit runs in
+ * the external kube-scheduler), so the placement entry points replace *that decision*; the
+ * ingest / demand / capacity entry points replace the Go functions cited on each declaration.
+ * The slurm-agent gRPC API (pkg/workload/workload.proto:23-62) and the virtual-kubelet provider
+ * interface (pkg/slurm-virtual-kubelet/provider.go:26) are unchanged; INTEGRATION.md shows the
+ * cgo binding and the call sites.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  The caller owns every buffer; the library copies inputs in
+ *     during the call and never retains a caller pointer (cgo rule).
+ *   - Return 0 on success, a negative FIT_E_* code on failure; fit_strerror() gives the text and
+ *     fit_last_error() the detail of the last failure on the calling thread.  No C++ exception
+ *     crosses the ABI.  There is no CPU fallback: without a usable gfx950 device fit_create fails.
+ *   - A fit_ctx must not be used by two threads at once; several contexts may coexist.
+ *   - Units: cpus, MiB, GPUs (gres/gpu count), minutes.  INT32_MAX avail = none.
+ */
+#ifndef FITGPU_H
+#define FITGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FITGPU_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------------------- */
+#define FIT_OK 0
+#define FIT_E_INVAL (-1)       /* invalid argument or input value                          */
+#define FIT_E_HIP (-2)         /* HIP runtime error                                        */
+#define FIT_E_RCCL (-3)        /* RCCL (collective) error                                  */
+#define FIT_E_OOM (-4)         /* device or host allocation failed                         */
+#define FIT_E_NODEV (-5)       /* no usable gfx950 device                                  */
+#define FIT_E_STATE (-6)       /* call out of order (e.g. fit_place before fit_load_nodes) */
+#define FIT_E_PARSE (-7)       /* malformed text (ingest helpers)                          */
+#define FIT_E_UNLIMITED (-8)   /* ParseDuration: ErrDurationIsUnlimited                    */
+
+/* ---- placement result codes (out_node entries) ------------------------------------------ */
+#define FIT_UNPLACED (-1)  /* no node (or not enough distinct nodes) fits at this point     */
+#define FIT_REJECTED (-2)  /* violates the partition's MaxTime/MaxCPUsPerNode/MaxMemPerNode  */
+
+#define FIT_MAX_PARTITIONS 32
+#define FIT_MAX_K 8         /* nodes per job (--nodes) supported by fit_place              */
+
+typedef struct fit_ctx fit_ctx;
+
+typedef struct {
+    int32_t device;       /* HIP device ordinal; -1 = current device                        */
+    int32_t rank;         /* this process' rank in a node-sharded group (0 if world == 1)  */
+    int32_t world;        /* number of GPUs sharing one placement (1 = single GPU)         */
+    const void* nccl_id;  /* 128-byte ncclUniqueId from fit_nccl_unique_id() when world>1 */
+    int32_t shard_mode;   /* 0 = auto, 1 = node-sharded (RCCL each round), 2 = partition-  */
+                          /*     component-sharded (no collective)                          */
+    int32_t window_min;   /* jobs per component per round, lower bound (0 = default 256)   */
+    int32_t window_max;   /* upper bound (0 = default 8192)                                 */
+    int32_t flags;        /* reserved, 0                                                    */
+} fit_opts;
+
+typedef struct {
+    int64_t jobs;          /* jobs in the call                                              */
+    int64_t placed;        /* jobs placed                                                    */
+    int64_t unplaced;      /* FIT_UNPLACED                                                   */
+    int64_t rejected;      /* FIT_REJECTED                                                   */
+    int64_t rounds;        /* speculative rounds executed                                    */
+    int64_t evals;         /* (job, node) fit evaluations performed by this rank's scans     */
+    int64_t useful_evals;  /* J_active × N: the single-pass work of the naive scalar path    */
+    int64_t stops_rescan;  /* round cut because a job's candidate list ran out               */
+    int64_t stops_dirty;   /* round cut because the dirty-node set was full                  */
+    double ms_total;       /* wall time of the call on the host clock                        */
+    double ms_scan;        /* device time in fit_scan (HIP events, summed over rounds)       */
+    double ms_commit;      /* device time in fit_commit                                      */
+    double ms_exchange;    /* device time in the RCCL exchange (world > 1)                   */
+} fit_stats;
+
+/* ---- engine -------------------------------------------------------------------------- */
+int fit_create(const fit_opts* opts, fit_ctx** out_ctx);
+void fit_destroy(fit_ctx* ctx);
+int fit_abi_version(void);
+const char* fit_strerror(int code);
+const char* fit_last_error(void);
+/* 128-byte RCCL unique id for a node-sharded group (rank 0 creates, everyone passes it). */
+int fit_nccl_unique_id(void* out128);
+
+/* Node table: one row per Slurm node, in Client.Nodes output order (pkg/slurm-agent/slurm.go:
+ * 343-364); the row index is the node id placements refer to.  free = total - alloc (the
+ * Node{Cpus,AlloCpus,Memory,AlloMemory,Gpus,AlloGpus} of workload.proto:165-174).  part_mask bit
+ * p = member of partition p.  Host pointers. */
+int fit_load_nodes(fit_ctx* ctx, int32_t n, const int32_t* cpu_free, const int32_t* mem_free,
+                   const int32_t* gpu_free, const int32_t* avail_min, const uint32_t* part_mask);
+/* Same, but the columns are device pointers (already resident in HBM on this context's GPU). */
+int fit_load_nodes_device(fit_ctx* ctx, int32_t n, const int32_t* cpu_free,
+                          const int32_t* mem_free, const int32_t* gpu_free,
+                          const int32_t* avail_min, const uint32_t* part_mask);
+
+/* Partition limits from parseResources (pkg/slurm-agent/parse.go:111-190) after the agent's
+ * override merge (pkg/slurm-agent/api/slurm.go:297-341): -1 = UNLIMITED.  Minutes / CPUs / MiB. */
+int fit_load_partitions(fit_ctx* ctx, int32_t p, const int32_t* max_time_min,
+                        const int32_t* max_cpus_per_node, const int32_t* max_mem_per_node);
+
+/* Place J jobs in priority order (index order) with sequential best-fit semantics.
+ * Demands are per node; nodes_k (may be NULL = all 1) is the --nodes count, 0 treated as 1.
+ * out_node[j*kmax + i], i < nodes_k[j]: node id, FIT_UNPLACED or FIT_REJECTED; other entries -1.
+ * The context's node table is updated (jobs consume resources).  Host pointers. */
+int fit_place(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+              const int32_t* wall, const uint16_t* part, const uint16_t* nodes_k, int32_t kmax,
+              int32_t* out_node, fit_stats* stats);
+/* Same with device pointers (inputs resident in HBM, output written in HBM). */
+int fit_place_device(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem,
+                     const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                     const uint16_t* nodes_k, int32_t kmax, int32_t* out_node, fit_stats* stats);
+
+/* Current (post-placement) free columns, in node-id order.  Host pointers, n entries each. */
+int fit_read_nodes(fit_ctx* ctx, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free);
+/* Free capacity per partition (Σ over member nodes of the current free columns): the engine's
+ * replacement for the allocation-blind sum of GetPartitionCapacity (node.go:183-190). */
+int fit_partition_free(fit_ctx* ctx, int32_t p, int64_t* cpu, int64_t* mem_mib, int64_t* gpu);
+
+/* ---- ingest / demand helpers (host code, mirrors of the reference Go functions) -------- */
+/* ParseDuration (pkg/slurm-agent/parse.go:36-109): 0 ok, FIT_E_UNLIMITED, FIT_E_PARSE. */
+int fit_parse_duration(const char* s, int64_t* out_ns);
+
+typedef struct {
+    int64_t nodes, mem_per_node, cpu_per_node, wall_ns;
+} fit_resources;
+/* parseResources (parse.go:111-190). */
+int fit_parse_resources(const char* text, fit_resources* out);
+
+typedef struct {
+    int64_t cpus, memory, gpus, allo_cpus, allo_memory, allo_gpus;
+} fit_node;
+/* Client.Nodes + parseNode (slurm.go:354-363, parse.go:291-308): parses `scontrol show nodes`
+ * text into at most cap records; returns the record count or a negative code. */
+int fit_parse_nodes(const char* text, fit_node* out, int32_t cap);
+/* parsePartition (parse.go:278-289): NUL-separated node names into buf; returns count. */
+int fit_parse_partition(const char* text, char* buf, int32_t buflen);
+/* parsePartitionsNames (parse.go:192-210): NUL-separated names into buf; returns count. */
+int fit_parse_partitions_names(const char* text, char* buf, int32_t buflen);
+
+typedef struct {
+    int64_t nodes, cpus_per_task, ntasks, ntasks_per_node, mem_per_cpu, wall_ns;
+    char array[64];
+} fit_job_resources;
+/* extractBatchResourcesFromScript (pkg/slurm-bridge-operator/parse.go:30-69): FIT_E_PARSE where
+ * the reference returns an error or panics (bare flag as the last #SBATCH token). */
+int fit_extract_batch_resources(const char* script, fit_job_resources* out);
+/* setRequireResourceBySpec + setDefaultRequireResource (pod.go:70-107). */
+void fit_apply_spec(fit_job_resources* r, int64_t nodes, int64_t cpus_per_task,
+                    int64_t mem_per_cpu, int64_t ntasks_per_node, const char* array,
+                    int64_t ntasks);
+/* parseArrayLen (parse.go:126-135). */
+int64_t fit_array_len(const char* array);
+/* genResourceListForPod (pod.go:143-162): the pod's cpu request and memory quantity (bytes). */
+void fit_pod_request(const fit_job_resources* r, int64_t* cpu, int64_t* memory);
+/* Engine demand vector for one (array task of a) job: DESIGN.md §2 "demand". */
+int fit_job_demand(const fit_job_resources* r, int32_t* cpu, int32_t* mem_mib, int32_t* wall_min,
+                   uint16_t* nodes_k);
+/* GetPartitionCapacity (pkg/slurm-virtual-kubelet/node.go:169-199), reference arithmetic. */
+void fit_partition_capacity(const fit_node* nodes, int32_t n, int64_t* cpu, int64_t* memory,
+                            int64_t* gpu, int64_t* pods);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FITGPU_H */

@@ -1,0 +1,636 @@
+// engine.cpp — host runtime of libfitgpu.so: context, node-table ingest into HBM, the
+// speculative round loop, node sharding over RCCL.  DESIGN.md §3.
+//
+// Boundary: include/fitgpu.h.  Everything here is plain C++ over the HIP runtime; the compute
+// is in fit_kernels.hip.  There is no CPU placement path: without a gfx950 device fit_create
+// fails with FIT_E_NODEV.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/fitgpu.h"
+#include "fit_device.h"
+
+namespace fitgpu {
+hipError_t launch_scan(int blocks, hipStream_t st, const NodeRec* rec, const int32_t* jl,
+                       const int32_t* jcpu, const int32_t* jmem, const int32_t* jgpu,
+                       const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
+                       const CompPlan* plan, int ncomp, uint64_t* cand, uint64_t* bnd,
+                       JobRec* wjob);
+hipError_t launch_commit(int ncomp, size_t lds_bytes, hipStream_t st, NodeRec* rec,
+                         const CompPlan* plan, const uint64_t* cand, int64_t rank_stride,
+                         int nranks, const uint64_t* bnd, const JobRec* wjob, int32_t* out,
+                         int kmax, CommitResult* res);
+hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* jmem,
+                            const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
+                            int32_t nj, int32_t kmax, const int32_t* ptab, int32_t np,
+                            int32_t* out, int8_t* jcomp);
+hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
+                               const int32_t* gpu, const int32_t* av, const uint32_t* mask,
+                               const int32_t* perm, int32_t nn, NodeRec* rec);
+hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, int32_t* cpu,
+                                int32_t* mem, int32_t* gpu);
+}  // namespace fitgpu
+
+using namespace fitgpu;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(FIT_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                                \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                      \
+    do {                                                                                    \
+        ncclResult_t r_ = (expr);                                                           \
+        if (r_ != ncclSuccess)                                                              \
+            return fail(FIT_E_RCCL, "%s failed: %s", #expr, ncclGetErrorString(r_));        \
+    } while (0)
+
+// device buffer that only grows
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 64);
+        if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            return fail(FIT_E_OOM, "hipMalloc(%zu bytes) failed", want * sizeof(T));
+        }
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+template <class T>
+struct HBuf {  // pinned host buffer
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 64);
+        if (hipHostMalloc(&p, want * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return fail(FIT_E_OOM, "hipHostMalloc(%zu bytes) failed", want * sizeof(T));
+        }
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+int find_root(int* par, int x) {
+    while (par[x] != x) x = par[x] = par[par[x]];
+    return x;
+}
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct fit_ctx {
+    int device = 0;
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[6] = {};
+    int wmin = 256, wmax = 8192;
+
+    // node table
+    int32_t n = 0;           // rows in caller order
+    int32_t nn = 0;          // rows in components (mask != 0)
+    int ncomp = 0;
+    int comp_of_part[32];
+    std::vector<int32_t> nb;  // ncomp + 1 component offsets (positions)
+    DBuf<NodeRec> rec;
+    DBuf<int32_t> col_cpu, col_mem, col_gpu, col_av, perm;
+    DBuf<uint32_t> col_mask;
+    std::vector<uint32_t> h_mask;
+    bool have_nodes = false;
+
+    // partitions: [max_time | max_cpus | max_mem | comp] × 32
+    int32_t np = 0;
+    int32_t ptab[128];
+    DBuf<int32_t> d_ptab;
+
+    // per-call scratch
+    DBuf<int32_t> jcpu, jmem, jgpu, jwall, out, jl;
+    DBuf<uint16_t> jpart, jk;
+    DBuf<int8_t> jcomp;
+    DBuf<uint64_t> cand, bnd;
+    DBuf<JobRec> wjob;
+    DBuf<CompPlan> plan;
+    DBuf<CommitResult> res;
+    HBuf<CompPlan> h_plan;
+    HBuf<CommitResult> h_res;
+    HBuf<int8_t> h_jcomp;
+    std::vector<int32_t> h_jl;
+
+    ~fit_ctx() {
+        for (auto* b : {&col_cpu, &col_mem, &col_gpu, &col_av, &perm, &jcpu, &jmem, &jgpu,
+                        &jwall, &out, &jl})
+            b->release();
+        rec.release();
+        col_mask.release();
+        d_ptab.release();
+        jpart.release();
+        jk.release();
+        jcomp.release();
+        cand.release();
+        bnd.release();
+        wjob.release();
+        plan.release();
+        res.release();
+        h_plan.release();
+        h_res.release();
+        h_jcomp.release();
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st) (void)hipStreamDestroy(st);
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+};
+
+namespace {
+
+int build_ptab(fit_ctx* c) {
+    for (int p = 0; p < 32; ++p) c->ptab[96 + p] = c->comp_of_part[p];
+    if (c->d_ptab.ensure(128)) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->d_ptab.p, c->ptab, sizeof c->ptab, hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
+// Components = partitions connected through nodes that belong to several of them; jobs of
+// different components never compete for a node, so each is an independent sequence
+// (DESIGN.md §3.1).  Nodes are laid out component by component, in id order inside each.
+int load_nodes_common(fit_ctx* c, int32_t n) {
+    int par[32];
+    for (int i = 0; i < 32; ++i) par[i] = i;
+    bool used[32] = {false};
+    for (int32_t x = 0; x < n; ++x) {
+        uint32_t m = c->h_mask[x];
+        if (!m) continue;
+        int lo = __builtin_ctz(m);
+        for (uint32_t r = m; r; r &= r - 1) {
+            int b = __builtin_ctz(r);
+            used[b] = true;
+            int ra = find_root(par, lo), rb = find_root(par, b);
+            if (ra != rb) par[std::max(ra, rb)] = std::min(ra, rb);
+        }
+    }
+    int root_comp[32];
+    for (int i = 0; i < 32; ++i) root_comp[i] = -1;
+    c->ncomp = 0;
+    for (int p = 0; p < 32; ++p) {
+        c->comp_of_part[p] = -1;
+        if (!used[p]) continue;
+        int r = find_root(par, p);
+        if (root_comp[r] < 0) root_comp[r] = c->ncomp++;
+        c->comp_of_part[p] = root_comp[r];
+    }
+    c->nb.assign(c->ncomp + 1, 0);
+    for (int32_t x = 0; x < n; ++x)
+        if (c->h_mask[x]) c->nb[c->comp_of_part[__builtin_ctz(c->h_mask[x])] + 1]++;
+    for (int k = 0; k < c->ncomp; ++k) {
+        if (c->nb[k + 1] > MAX_COMPONENT_NODES)
+            return fail(FIT_E_INVAL, "partition component %d has %d nodes (limit %d)", k,
+                        c->nb[k + 1], MAX_COMPONENT_NODES);
+        c->nb[k + 1] += c->nb[k];
+    }
+    c->nn = c->nb[c->ncomp];
+    std::vector<int32_t> fill(c->nb.begin(), c->nb.end() - 1), perm(std::max(c->nn, 1));
+    for (int32_t x = 0; x < n; ++x)
+        if (c->h_mask[x]) perm[fill[c->comp_of_part[__builtin_ctz(c->h_mask[x])]]++] = x;
+    if (c->perm.ensure(std::max(c->nn, 1)) || c->rec.ensure(std::max(c->nn, 1))) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->perm.p, perm.data(), sizeof(int32_t) * c->nn, hipMemcpyHostToDevice,
+                           c->st));
+    HIP_TRY(launch_gather_nodes(c->st, c->col_cpu.p, c->col_mem.p, c->col_gpu.p, c->col_av.p,
+                                c->col_mask.p, c->perm.p, c->nn, c->rec.p));
+    int rc = build_ptab(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    c->n = n;
+    c->have_nodes = true;
+    return 0;
+}
+
+int alloc_cols(fit_ctx* c, int32_t n) {
+    size_t m = std::max<int32_t>(n, 1);
+    if (c->col_cpu.ensure(m) || c->col_mem.ensure(m) || c->col_gpu.ensure(m) ||
+        c->col_av.ensure(m) || c->col_mask.ensure(m))
+        return FIT_E_OOM;
+    return 0;
+}
+
+// ------------------------------------------------------------------------ placement
+int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+               const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
+               int32_t* out, fit_stats* stats) {
+    const double t0 = now_ms();
+    fit_stats S;
+    memset(&S, 0, sizeof S);
+    S.jobs = J;
+    hipStream_t st = c->st;
+    // 1. prefilter: out[] init, FIT_REJECTED, component per job
+    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    HIP_TRY(launch_prefilter(st, cpu, mem, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
+                             c->jcomp.p));
+    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // 2. per-component job lists in priority order (stable)
+    const int C = c->ncomp;
+    std::vector<int32_t> jb(C + 1, 0);
+    for (int32_t q = 0; q < J; ++q) {
+        int8_t k = c->h_jcomp.p[q];
+        if (k >= 0) jb[k + 1]++;
+        else if (k == -2) S.rejected++;
+    }
+    for (int k = 0; k < C; ++k) jb[k + 1] += jb[k];
+    const int32_t JA = jb[C];
+    c->h_jl.resize(std::max(JA, 1));
+    {
+        std::vector<int32_t> f(jb.begin(), jb.end() - 1);
+        for (int32_t q = 0; q < J; ++q) {
+            int8_t k = c->h_jcomp.p[q];
+            if (k >= 0) c->h_jl[f[k]++] = q;
+        }
+    }
+    if (c->jl.ensure(std::max(JA, 1))) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->jl.p, c->h_jl.data(), sizeof(int32_t) * JA, hipMemcpyHostToDevice,
+                           st));
+    for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
+
+    // 3. speculative rounds
+    std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
+    if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||
+        c->h_res.ensure(C + 1))
+        return FIT_E_OOM;
+    float ms;
+    for (;;) {
+        int64_t blocks = 0, slots = 0, cand_n = 0, evals = 0;
+        size_t lds = 0;
+        bool any = false;
+        for (int k = 0; k < C; ++k) {
+            CompPlan& P = c->h_plan.p[k];
+            memset(&P, 0, sizeof P);
+            P.nb = c->nb[k];
+            P.ne = c->nb[k + 1];
+            const int32_t len = P.ne - P.nb;
+            const int32_t per = (len + c->world - 1) / c->world;
+            P.sb = std::min(P.ne, P.nb + per * c->rank);
+            P.se = std::min(P.ne, P.sb + per);
+            P.nslice = std::max(1, (per + SLICE - 1) / SLICE);
+            P.jbase = cur[k];
+            P.w = std::min(win[k], jb[k + 1] - cur[k]);
+            P.blk0 = (int32_t)blocks;
+            P.cand_off = cand_n;
+            P.slot0 = (int32_t)slots;
+            if (P.w > 0) {
+                any = true;
+                blocks += (int64_t)((P.w + SCAN_BLOCK - 1) / SCAN_BLOCK) * P.nslice;
+                cand_n += (int64_t)P.w * P.nslice * KS;
+                slots += P.w;
+                evals += (int64_t)P.w * (P.se - P.sb);
+                lds = std::max(lds, (size_t)((len + 31) / 32) * 4);
+            }
+        }
+        if (!any) break;
+        S.rounds++;
+        S.evals += evals;
+        if (c->cand.ensure((size_t)cand_n * c->world) || c->bnd.ensure(slots) ||
+            c->wjob.ensure(slots))
+            return FIT_E_OOM;
+        HIP_TRY(hipMemcpyAsync(c->plan.p, c->h_plan.p, sizeof(CompPlan) * C, hipMemcpyHostToDevice,
+                               st));
+        HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * slots, st));
+        HIP_TRY(hipEventRecord(c->ev[0], st));
+        HIP_TRY(launch_scan((int)blocks, st, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
+                            c->plan.p, C, c->cand.p + (size_t)c->rank * cand_n, c->bnd.p,
+                            c->wjob.p));
+        HIP_TRY(hipEventRecord(c->ev[1], st));
+        if (c->world > 1) {
+            // every rank scanned its node shard: gather all candidate sections, min the bounds
+            NCCL_TRY(ncclAllGather(c->cand.p + (size_t)c->rank * cand_n, c->cand.p, cand_n,
+                                   ncclUint64, c->comm, st));
+            NCCL_TRY(ncclAllReduce(c->bnd.p, c->bnd.p, slots, ncclUint64, ncclMin, c->comm, st));
+        }
+        HIP_TRY(hipEventRecord(c->ev[2], st));
+        HIP_TRY(launch_commit(C, lds, st, c->rec.p, c->plan.p, c->cand.p, cand_n, c->world,
+                              c->bnd.p, c->wjob.p, out, kmax, c->res.p));
+        HIP_TRY(hipEventRecord(c->ev[3], st));
+        HIP_TRY(hipMemcpyAsync(c->h_res.p, c->res.p, sizeof(CommitResult) * C,
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        S.ms_scan += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        S.ms_exchange += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        S.ms_commit += ms;
+        for (int k = 0; k < C; ++k) {
+            const CompPlan& P = c->h_plan.p[k];
+            if (P.w == 0) continue;
+            const CommitResult& R = c->h_res.p[k];
+            if (R.done < 0 || R.done > P.w)
+                return fail(FIT_E_HIP, "commit returned %d of window %d", R.done, P.w);
+            cur[k] += R.done;
+            S.placed += R.placed;
+            if (R.stop == 1) S.stops_rescan++;
+            if (R.stop == 2) S.stops_dirty++;
+            int32_t nw = R.stop ? 2 * R.done : 2 * P.w;
+            win[k] = std::max(c->wmin, std::min(c->wmax, nw));
+        }
+    }
+    // jobs of partitions without nodes are FIT_UNPLACED like jobs nothing fits
+    S.unplaced = J - S.placed - S.rejected;
+    S.ms_total = now_ms() - t0;
+    if (stats) *stats = S;
+    return 0;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+int fit_abi_version(void) { return FITGPU_ABI_VERSION; }
+
+const char* fit_strerror(int code) {
+    switch (code) {
+        case FIT_OK: return "ok";
+        case FIT_E_INVAL: return "invalid argument";
+        case FIT_E_HIP: return "HIP runtime error";
+        case FIT_E_RCCL: return "RCCL error";
+        case FIT_E_OOM: return "out of memory";
+        case FIT_E_NODEV: return "no usable gfx950 device";
+        case FIT_E_STATE: return "call out of order";
+        case FIT_E_PARSE: return "parse error";
+        case FIT_E_UNLIMITED: return "duration is unlimited";
+        default: return "unknown error";
+    }
+}
+
+const char* fit_last_error(void) { return g_last_error.c_str(); }
+
+int fit_nccl_unique_id(void* out128) {
+    if (!out128) return fail(FIT_E_INVAL, "null id buffer");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out128, &id, sizeof id);
+    return 0;
+}
+
+int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
+    if (!out_ctx) return fail(FIT_E_INVAL, "null out_ctx");
+    *out_ctx = nullptr;
+    fit_opts o;
+    memset(&o, 0, sizeof o);
+    o.device = -1;
+    o.world = 1;
+    if (opts) o = *opts;
+    if (o.world < 1 || o.rank < 0 || o.rank >= o.world)
+        return fail(FIT_E_INVAL, "rank %d / world %d", o.rank, o.world);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FIT_E_NODEV, "no HIP device visible");
+    int dev = o.device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev >= ndev) return fail(FIT_E_INVAL, "device %d of %d", dev, ndev);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(FIT_E_NODEV, "device %d is %s, this build targets gfx950", dev,
+                    prop.gcnArchName);
+    HIP_TRY(hipSetDevice(dev));
+    fit_ctx* c = new (std::nothrow) fit_ctx();
+    if (!c) return fail(FIT_E_OOM, "context allocation");
+    c->device = dev;
+    c->rank = o.rank;
+    c->world = o.world;
+    if (o.window_min > 0) c->wmin = o.window_min;
+    if (o.window_max > 0) c->wmax = std::max(o.window_max, c->wmin);
+    for (int p = 0; p < 32; ++p) {
+        c->comp_of_part[p] = -1;
+        c->ptab[p] = c->ptab[32 + p] = c->ptab[64 + p] = -1;
+        c->ptab[96 + p] = -1;
+    }
+    int rc = 0;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) rc = FIT_E_HIP;
+    for (auto& e : c->ev)
+        if (!rc && hipEventCreate(&e) != hipSuccess) rc = FIT_E_HIP;
+    if (!rc && c->world > 1) {
+        if (!o.nccl_id) {
+            rc = fail(FIT_E_INVAL, "world > 1 needs nccl_id");
+        } else {
+            ncclUniqueId id;
+            memcpy(&id, o.nccl_id, sizeof id);
+            ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
+            if (r != ncclSuccess)
+                rc = fail(FIT_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+    } else if (rc) {
+        fail(rc, "stream/event creation failed");
+    }
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    *out_ctx = c;
+    return 0;
+}
+
+void fit_destroy(fit_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->st);
+    delete ctx;
+}
+
+int fit_load_nodes(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem,
+                   const int32_t* gpu, const int32_t* av, const uint32_t* mask) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (n < 0 || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
+        return fail(FIT_E_INVAL, "bad node arrays");
+    HIP_TRY(hipSetDevice(c->device));
+    if (alloc_cols(c, n)) return FIT_E_OOM;
+    const size_t b = sizeof(int32_t) * n;
+    HIP_TRY(hipMemcpyAsync(c->col_cpu.p, cpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_mem.p, mem, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_gpu.p, gpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_av.p, av, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_mask.p, mask, b, hipMemcpyHostToDevice, c->st));
+    c->h_mask.assign(mask, mask + n);
+    return load_nodes_common(c, n);
+}
+
+int fit_load_nodes_device(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem,
+                          const int32_t* gpu, const int32_t* av, const uint32_t* mask) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (n < 0 || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
+        return fail(FIT_E_INVAL, "bad node arrays");
+    HIP_TRY(hipSetDevice(c->device));
+    if (alloc_cols(c, n)) return FIT_E_OOM;
+    const size_t b = sizeof(int32_t) * n;
+    HIP_TRY(hipMemcpyAsync(c->col_cpu.p, cpu, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_mem.p, mem, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_gpu.p, gpu, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_av.p, av, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->col_mask.p, mask, b, hipMemcpyDeviceToDevice, c->st));
+    c->h_mask.resize(n);
+    HIP_TRY(hipMemcpyAsync(c->h_mask.data(), mask, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return load_nodes_common(c, n);
+}
+
+int fit_load_partitions(fit_ctx* c, int32_t p, const int32_t* max_time,
+                        const int32_t* max_cpus, const int32_t* max_mem) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (p < 0 || p > FIT_MAX_PARTITIONS || (p > 0 && (!max_time || !max_cpus || !max_mem)))
+        return fail(FIT_E_INVAL, "bad partition table (p=%d)", p);
+    HIP_TRY(hipSetDevice(c->device));
+    c->np = p;
+    for (int i = 0; i < 32; ++i) {
+        c->ptab[i] = i < p ? max_time[i] : -1;
+        c->ptab[32 + i] = i < p ? max_cpus[i] : -1;
+        c->ptab[64 + i] = i < p ? max_mem[i] : -1;
+    }
+    int rc = build_ptab(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+static int check_place_args(fit_ctx* c, int32_t j, const void* a, const void* b, const void* d,
+                            const void* e, const void* f, int32_t kmax, const void* out) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
+    if (j < 0 || (j > 0 && (!a || !b || !d || !e || !f || !out)))
+        return fail(FIT_E_INVAL, "bad job arrays");
+    if (kmax != 1)
+        return fail(FIT_E_INVAL, "kmax=%d: multi-node jobs are not enabled in this build", kmax);
+    return 0;
+}
+
+int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+              const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
+              int32_t* out, fit_stats* stats) {
+    int rc = check_place_args(c, j, cpu, mem, gpu, wall, part, kmax, out);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    for (int32_t q = 0; q < j; ++q)
+        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0 ||
+            (nk && std::max<int>(nk[q], 1) > kmax))
+            return fail(FIT_E_INVAL, "job %d: negative demand or nodes_k > kmax", q);
+    size_t m = std::max(j, 1);
+    if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
+        c->jpart.ensure(m) || c->jk.ensure(m) || c->out.ensure(m * kmax))
+        return FIT_E_OOM;
+    const size_t b = sizeof(int32_t) * j;
+    HIP_TRY(hipMemcpyAsync(c->jcpu.p, cpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jmem.p, mem, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jgpu.p, gpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jwall.p, wall, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jpart.p, part, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
+    if (nk)
+        HIP_TRY(hipMemcpyAsync(c->jk.p, nk, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
+    rc = place_impl(c, j, c->jcpu.p, c->jmem.p, c->jgpu.p, c->jwall.p, c->jpart.p,
+                    nk ? c->jk.p : nullptr, kmax, c->out.p, stats);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->out.p, sizeof(int32_t) * j * kmax, hipMemcpyDeviceToHost,
+                           c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int fit_place_device(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem,
+                     const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                     const uint16_t* nk, int32_t kmax, int32_t* out, fit_stats* stats) {
+    int rc = check_place_args(c, j, cpu, mem, gpu, wall, part, kmax, out);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    rc = place_impl(c, j, cpu, mem, gpu, wall, part, nk, kmax, out, stats);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int fit_read_nodes(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
+    if (c->n > 0 && (!cpu || !mem || !gpu)) return fail(FIT_E_INVAL, "null output");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_scatter_nodes(c->st, c->rec.p, c->nn, c->col_cpu.p, c->col_mem.p,
+                                 c->col_gpu.p));
+    const size_t b = sizeof(int32_t) * c->n;
+    HIP_TRY(hipMemcpyAsync(cpu, c->col_cpu.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(mem, c->col_mem.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(gpu, c->col_gpu.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int fit_partition_free(fit_ctx* c, int32_t p, int64_t* cpu, int64_t* mem, int64_t* gpu) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (p < 0 || p >= 32 || !cpu || !mem || !gpu) return fail(FIT_E_INVAL, "bad partition");
+    std::vector<int32_t> hc(c->n), hm(c->n), hg(c->n);
+    int rc = fit_read_nodes(c, hc.data(), hm.data(), hg.data());
+    if (rc) return rc;
+    int64_t sc = 0, sm = 0, sg = 0;
+    for (int32_t x = 0; x < c->n; ++x)
+        if ((c->h_mask[x] >> p) & 1u) {
+            sc += std::max(hc[x], 0);
+            sm += std::max(hm[x], 0);
+            sg += std::max(hg[x], 0);
+        }
+    *cpu = sc;
+    *mem = sm;
+    *gpu = sg;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+// fit_device.h — data layouts shared by the HIP kernels and the host engine.
+#pragma once
+#include <stdint.h>
+
+namespace fitgpu {
+
+constexpr int KS = 16;          // candidates kept per (job, node slice) by fit_scan
+constexpr int SLICE = 2048;     // nodes per scan slice (one scan block walks one slice)
+constexpr int UCAP = 256;       // dirty-node capacity per component per round (4 per lane)
+constexpr int SCAN_BLOCK = 256; // jobs per scan block (4 waves, lanes = jobs)
+constexpr int MAX_COMPONENT_NODES = 1 << 20;  // LDS dirty bitmap limit (128 KiB)
+constexpr uint64_t KEY_INF = ~0ull;
+
+// One Slurm node row in HBM, 32 B: read by fit_scan with one scalar s_load_dwordx8.
+struct alignas(32) NodeRec {
+    int32_t cpu, mem, gpu, avail;  // free cpus, free MiB, free GPUs, availability horizon (min)
+    uint32_t mask;                 // partition membership bits
+    int32_t orig;                  // node id in the caller's order (Client.Nodes order)
+    int32_t pad0, pad1;
+};
+
+// Job row of the current window, written by fit_scan (slice 0), read by fit_commit.
+struct alignas(32) JobRec {
+    int32_t q;        // job index in the caller's priority order
+    int32_t cpu, mem, gpu, wall;
+    uint32_t pbit;    // 1u << partition
+    int32_t k;        // nodes per job
+    int32_t pad;
+};
+
+// Per-component plan for one round (host-built, uploaded each round).
+struct alignas(16) CompPlan {
+    int32_t nb, ne;      // component's node positions [nb, ne)
+    int32_t sb, se;      // this rank's scan range inside it
+    int32_t nslice;      // slices per job on every rank
+    int32_t jbase;       // first window job's index into the component job list
+    int32_t w;           // window size (jobs)
+    int32_t blk0;        // first fit_scan block of this component
+    int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
+    int32_t slot0;       // first window slot (global over components)
+    int32_t pad;
+};
+
+struct CommitResult {
+    int32_t done;   // jobs resolved this round (prefix of the window)
+    int32_t stop;   // 0 window exhausted, 1 candidate list ran out, 2 dirty set full
+    int32_t dirty;  // distinct nodes touched
+    int32_t placed;
+};
+
+}  // namespace fitgpu

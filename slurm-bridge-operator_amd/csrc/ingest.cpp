@@ -1,0 +1,393 @@
+// ingest.cpp — host-side mirrors of the reference's text ingest and demand arithmetic that feed
+// the placement engine.  Same names, argument meaning and error
+// behaviour as the Go functions cited on each; one deliberate difference: where the reference
+// panics (a bare flag as the last #SBATCH token, pkg/slurm-bridge-operator/parse.go:58-60) this
+// returns FIT_E_PARSE.  Text is handled as ASCII (scontrol output is ASCII).
+#include <cstdint>
+#include <cstring>
+#include <string_view>
+#include <vector>
+
+#include "../../include/fitgpu.h"
+
+namespace {
+
+using sv = std::string_view;
+
+bool is_space(char c) {
+    return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r';
+}
+
+sv trim_space(sv s) {  // strings.TrimSpace
+    while (!s.empty() && is_space(s.front())) s.remove_prefix(1);
+    while (!s.empty() && is_space(s.back())) s.remove_suffix(1);
+    return s;
+}
+
+std::vector<sv> fields(sv s) {  // strings.Fields
+    std::vector<sv> out;
+    size_t i = 0;
+    while (i < s.size()) {
+        while (i < s.size() && is_space(s[i])) ++i;
+        size_t b = i;
+        while (i < s.size() && !is_space(s[i])) ++i;
+        if (i > b) out.push_back(s.substr(b, i - b));
+    }
+    return out;
+}
+
+std::vector<sv> split(sv s, sv sep) {  // strings.Split (sep non-empty)
+    std::vector<sv> out;
+    size_t b = 0;
+    for (;;) {
+        size_t p = s.find(sep, b);
+        if (p == sv::npos) {
+            out.push_back(s.substr(b));
+            return out;
+        }
+        out.push_back(s.substr(b, p - b));
+        b = p + sep.size();
+    }
+}
+
+// strconv.ParseInt(s, 10, 64): 0 ok, 1 syntax error (v = 0), 2 range error (v clamped)
+int parse_int(sv s, int64_t& v) {
+    v = 0;
+    if (s.empty()) return 1;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') {
+        neg = s[0] == '-';
+        s.remove_prefix(1);
+        if (s.empty()) return 1;
+    }
+    const uint64_t lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+    uint64_t acc = 0;
+    bool over = false;
+    for (char ch : s) {
+        if (ch < '0' || ch > '9') {
+            v = 0;
+            return 1;
+        }
+        const uint64_t d = (uint64_t)(ch - '0');
+        if (!over && acc > (lim - d) / 10) over = true;
+        if (!over) acc = acc * 10 + d;
+    }
+    if (over) {
+        v = neg ? INT64_MIN : INT64_MAX;
+        return 2;
+    }
+    v = neg ? (int64_t)(0 - acc) : (int64_t)acc;
+    return 0;
+}
+
+// ParseDuration, pkg/slurm-agent/parse.go:36-109
+int parse_duration(sv d, int64_t& ns) {
+    ns = 0;
+    if (d == "UNLIMITED" || d.empty()) return FIT_E_UNLIMITED;
+    const std::vector<sv> parts = split(d, ":");
+    if (parts.size() > 3) return FIT_E_PARSE;
+    int64_t days = 0, hours = 0, minutes = 0, seconds = 0;
+    const size_t i = parts[0].find('-');
+    if (i != sv::npos) {
+        if (parse_int(parts[0].substr(0, i), days)) return FIT_E_PARSE;
+        if (parse_int(parts[0].substr(i + 1), hours)) return FIT_E_PARSE;
+        if (parts.size() > 1 && parse_int(parts[1], minutes)) return FIT_E_PARSE;
+        if (parts.size() > 2 && parse_int(parts[2], seconds)) return FIT_E_PARSE;
+    } else if (parts.size() == 1) {
+        if (parse_int(parts[0], minutes)) return FIT_E_PARSE;
+    } else if (parts.size() == 2) {
+        if (parse_int(parts[0], minutes) || parse_int(parts[1], seconds)) return FIT_E_PARSE;
+    } else {
+        if (parse_int(parts[0], hours) || parse_int(parts[1], minutes) ||
+            parse_int(parts[2], seconds))
+            return FIT_E_PARSE;
+    }
+    constexpr uint64_t S = 1000000000ull, M = 60 * S, H = 60 * M;
+    uint64_t acc = 24 * H * (uint64_t)days;  // time.Duration arithmetic wraps
+    acc += H * (uint64_t)hours;
+    acc += M * (uint64_t)minutes;
+    acc += S * (uint64_t)seconds;
+    ns = (int64_t)acc;
+    return FIT_OK;
+}
+
+// value of the first "key=v1,v2,..." field (fMap[key][0] in parseResources), if present
+bool first_value(const std::vector<sv>& fs, sv key, sv& out) {
+    for (sv f : fs) {
+        const std::vector<sv> kv = split(f, "=");
+        if (kv.size() != 2 || kv[0] != key) continue;
+        out = split(kv[1], ",")[0];
+        return true;
+    }
+    return false;
+}
+
+int put_names(const std::vector<sv>& names, char* buf, int32_t buflen) {
+    int32_t used = 0;
+    for (sv s : names) {
+        if (used + (int32_t)s.size() + 1 > buflen) return FIT_E_INVAL;
+        if (!s.empty()) memcpy(buf + used, s.data(), s.size());
+        buf[used + s.size()] = 0;
+        used += (int32_t)s.size() + 1;
+    }
+    return (int)names.size();
+}
+
+void parse_node(sv raw, fit_node& n) {  // parseNode, parse.go:291-308
+    n = fit_node{};
+    for (sv f : fields(raw)) {
+        const std::vector<sv> kv = split(f, "=");
+        if (kv.size() != 2) continue;
+        int64_t v;
+        if (kv[0] == "CPUTot") {
+            parse_int(kv[1], v);  // errors ignored (`_ =`), value as ParseInt returns it
+            n.cpus = v;
+        } else if (kv[0] == "CPUAlloc") {
+            parse_int(kv[1], v);
+            n.allo_cpus = v;
+        } else if (kv[0] == "RealMemory") {
+            parse_int(kv[1], v);
+            n.memory = v;
+        } else if (kv[0] == "AllocMem") {
+            parse_int(kv[1], v);
+            n.allo_memory = v;
+        }
+    }
+}
+
+// applySbatchParam, pkg/slurm-bridge-operator/parse.go:82-124
+int apply_sbatch_param(fit_job_resources& r, sv param, sv value) {
+    int64_t v;
+    if (param == "--time" || param == "-t") {
+        int64_t ns;
+        const int rc = parse_duration(value, ns);
+        if (rc == FIT_E_PARSE) return FIT_E_PARSE;
+        if (rc == FIT_OK) r.wall_ns = ns;
+    } else if (param == "--nodes" || param == "-N") {
+        const size_t i = value.find('-');  // min nodes only
+        if (i != sv::npos) value = value.substr(0, i);
+        if (parse_int(value, v)) return FIT_E_PARSE;
+        r.nodes = v;
+    } else if (param == "--mem-per-cpu") {
+        if (parse_int(value, v)) return FIT_E_PARSE;
+        r.mem_per_cpu = v;
+    } else if (param == "--cpus-per-task" || param == "-c") {
+        if (parse_int(value, v)) return FIT_E_PARSE;
+        r.cpus_per_task = v;
+    } else if (param == "--ntasks-per-node") {
+        if (parse_int(value, v)) return FIT_E_PARSE;
+        r.ntasks_per_node = v;
+    }
+    return FIT_OK;
+}
+
+int64_t atoi_go(sv s) {  // strconv.Atoi value as returned alongside an error
+    int64_t v;
+    return parse_int(s, v) == 1 ? 0 : v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fit_parse_duration(const char* s, int64_t* out_ns) {
+    if (!s || !out_ns) return FIT_E_INVAL;
+    return parse_duration(sv(s), *out_ns);
+}
+
+int fit_parse_resources(const char* text, fit_resources* out) {  // parse.go:111-190
+    if (!text || !out) return FIT_E_INVAL;
+    *out = fit_resources{};
+    const std::vector<sv> fs = fields(trim_space(sv(text)));
+    sv v, tot;
+    if (first_value(fs, "MaxTime", v)) {
+        int64_t ns;
+        const int rc = parse_duration(v, ns);
+        if (rc == FIT_E_PARSE) return FIT_E_PARSE;
+        out->wall_ns = rc == FIT_E_UNLIMITED ? -1 : ns;
+    }
+    int64_t x;
+    if (first_value(fs, "MaxCPUsPerNode", v)) {
+        if (v == "UNLIMITED") {
+            out->cpu_per_node = -1;
+            if (first_value(fs, "TotalCPUs", tot)) {
+                if (parse_int(tot, x)) return FIT_E_PARSE;
+                out->cpu_per_node = x;
+            }
+        } else {
+            if (parse_int(v, x)) return FIT_E_PARSE;
+            out->cpu_per_node = x;
+        }
+    }
+    if (first_value(fs, "MaxMemPerNode", v)) {
+        if (v == "UNLIMITED") {
+            out->mem_per_node = -1;
+        } else {
+            if (parse_int(v, x)) return FIT_E_PARSE;
+            out->mem_per_node = x;
+        }
+    }
+    if (first_value(fs, "MaxNodes", v)) {
+        if (v == "UNLIMITED") {
+            out->nodes = -1;
+            if (first_value(fs, "TotalNodes", tot)) {
+                if (parse_int(tot, x)) return FIT_E_PARSE;
+                out->nodes = x;
+            }
+        } else {
+            if (parse_int(v, x)) return FIT_E_PARSE;
+            out->nodes = x;
+        }
+    }
+    return FIT_OK;
+}
+
+int fit_parse_nodes(const char* text, fit_node* out, int32_t cap) {  // slurm.go:354-363
+    if (!text || (cap > 0 && !out) || cap < 0) return FIT_E_INVAL;
+    int32_t n = 0;
+    for (sv rec : split(trim_space(sv(text)), "\n\n")) {
+        if (rec.empty()) continue;
+        if (n == cap) return FIT_E_INVAL;
+        parse_node(rec, out[n++]);
+    }
+    return n;
+}
+
+int fit_parse_partition(const char* text, char* buf, int32_t buflen) {  // parse.go:278-289
+    if (!text || !buf) return FIT_E_INVAL;
+    std::vector<sv> nodes;
+    for (sv f : fields(sv(text))) {
+        const std::vector<sv> kv = split(f, "=");
+        if (kv.size() == 2 && kv[0] == "Nodes")
+            for (sv n : split(kv[1], ",")) nodes.push_back(n);
+    }
+    return put_names(nodes, buf, buflen);
+}
+
+int fit_parse_partitions_names(const char* text, char* buf, int32_t buflen) {  // :192-210
+    if (!text || !buf) return FIT_E_INVAL;
+    std::vector<sv> names;
+    for (sv p : split(trim_space(sv(text)), "\n\n")) {
+        sv name;
+        for (sv f : fields(p)) {
+            const std::vector<sv> kv = split(f, "=");
+            if (kv.size() == 2 && kv[0] == "PartitionName") name = kv[1];
+        }
+        names.push_back(name);
+    }
+    return put_names(names, buf, buflen);
+}
+
+int fit_extract_batch_resources(const char* script, fit_job_resources* out) {  // parse.go:30-69
+    if (!script || !out) return FIT_E_INVAL;
+    *out = fit_job_resources{};
+    sv rest(script);
+    while (!rest.empty()) {  // bufio.Scanner / ScanLines
+        const size_t nl = rest.find('\n');
+        sv line = rest.substr(0, nl);
+        rest = nl == sv::npos ? sv() : rest.substr(nl + 1);
+        if (!line.empty() && line.back() == '\r') line.remove_suffix(1);
+        if (line.size() > 64 * 1024) break;  // bufio.ErrTooLong stops the scan
+        if (line.empty() || line.substr(0, 2) == "#!") continue;
+        if (line.substr(0, 7) != "#SBATCH") break;
+        const std::vector<sv> params = fields(line.substr(7));
+        for (size_t j = 0; j < params.size(); ++j) {
+            sv param = params[j], value;
+            const size_t i = param.find('=');
+            if (i != sv::npos) {
+                value = param.substr(i + 1);
+                param = param.substr(0, i);
+            } else {
+                // the reference always takes params[j+1] here (`i < len(params)-1`, i == -1)
+                if (j + 1 >= params.size()) return FIT_E_PARSE;  // reference: index panic
+                value = params[++j];
+            }
+            const int rc = apply_sbatch_param(*out, param, value);
+            if (rc) return rc;
+        }
+    }
+    return FIT_OK;
+}
+
+void fit_apply_spec(fit_job_resources* r, int64_t nodes, int64_t cpus_per_task,
+                    int64_t mem_per_cpu, int64_t ntasks_per_node, const char* array,
+                    int64_t ntasks) {  // pod.go:70-107
+    if (!r) return;
+    if (nodes > 0) r->nodes = nodes;
+    if (cpus_per_task > 0) r->cpus_per_task = cpus_per_task;
+    if (mem_per_cpu > 0) r->mem_per_cpu = mem_per_cpu;
+    if (ntasks_per_node > 0) r->ntasks_per_node = ntasks_per_node;
+    if (array && array[0]) {
+        const size_t n = std::min(strlen(array), sizeof(r->array) - 1);
+        memcpy(r->array, array, n);
+        r->array[n] = 0;
+    }
+    if (ntasks > 0) r->ntasks = ntasks;
+    if (r->nodes == 0) r->nodes = 1;
+    if (r->cpus_per_task == 0) r->cpus_per_task = 1;
+    if (r->mem_per_cpu == 0) r->mem_per_cpu = 1024;
+}
+
+int64_t fit_array_len(const char* array) {  // parse.go:126-135
+    if (!array) return 0;
+    const sv a(array);
+    if (a.find('-') != sv::npos) {
+        const std::vector<sv> s = split(a, "-");
+        return (int64_t)((uint64_t)atoi_go(s[1]) - (uint64_t)atoi_go(s[0]) + 1);
+    }
+    return (int64_t)split(a, ",").size();
+}
+
+void fit_pod_request(const fit_job_resources* r, int64_t* cpu, int64_t* memory) {  // :143-162
+    if (!r || !cpu || !memory) return;
+    uint64_t n;
+    if (r->ntasks > 0)
+        n = (uint64_t)r->cpus_per_task * (uint64_t)r->ntasks;
+    else if (r->ntasks_per_node > 0 && r->nodes > 0)
+        n = (uint64_t)r->cpus_per_task * (uint64_t)r->ntasks_per_node * (uint64_t)r->nodes;
+    else
+        n = (uint64_t)r->cpus_per_task;
+    if (r->array[0]) n *= (uint64_t)fit_array_len(r->array);
+    *cpu = (int64_t)n;
+    *memory = (int64_t)(n * (uint64_t)r->mem_per_cpu * 1024u);
+}
+
+int fit_job_demand(const fit_job_resources* r, int32_t* cpu, int32_t* mem_mib, int32_t* wall_min,
+                   uint16_t* nodes_k) {
+    // DESIGN.md §2 "demand": per-node cpus = cpusPerTask × tasks per node, where tasks per node =
+    // ntasksPerNode, else ceil(ntasks / nodes), else 1; mem = cpus × memPerCpu (MiB, Slurm's
+    // --mem-per-cpu unit); walltime rounded up to whole minutes; nodes = --nodes (min).
+    if (!r || !cpu || !mem_mib || !wall_min || !nodes_k) return FIT_E_INVAL;
+    const int64_t k = r->nodes > 0 ? r->nodes : 1;
+    int64_t tpn = 1;
+    if (r->ntasks_per_node > 0) tpn = r->ntasks_per_node;
+    else if (r->ntasks > 0) tpn = (r->ntasks + k - 1) / k;
+    const int64_t cpt = r->cpus_per_task > 0 ? r->cpus_per_task : 1;
+    const int64_t mpc = r->mem_per_cpu > 0 ? r->mem_per_cpu : 1024;
+    if (k > 65535 || tpn > INT32_MAX || cpt > INT32_MAX || tpn * cpt > INT32_MAX ||
+        mpc > INT32_MAX || tpn * cpt * mpc > INT32_MAX || r->wall_ns < 0)
+        return FIT_E_INVAL;
+    const int64_t w = (r->wall_ns + 59999999999ll) / 60000000000ll;
+    if (w > INT32_MAX) return FIT_E_INVAL;
+    *cpu = (int32_t)(tpn * cpt);
+    *mem_mib = (int32_t)(tpn * cpt * mpc);
+    *wall_min = (int32_t)w;
+    *nodes_k = (uint16_t)k;
+    return FIT_OK;
+}
+
+void fit_partition_capacity(const fit_node* nodes, int32_t n, int64_t* cpu, int64_t* memory,
+                            int64_t* gpu, int64_t* pods) {  // node.go:169-199
+    uint64_t c = 0, m = 0, g = 0;
+    for (int32_t i = 0; nodes && i < n; ++i) {
+        c += (uint64_t)nodes[i].cpus;
+        m += (uint64_t)nodes[i].memory;
+        g += (uint64_t)nodes[i].gpus;
+    }
+    if (cpu) *cpu = (int64_t)c;
+    if (memory) *memory = (int64_t)(m * (2u << 10));  // node.go:193 — MiB × 2048, as the ref
+    if (gpu) *gpu = (int64_t)g;
+    if (pods) *pods = (int64_t)c;  // node.go:197
+}
+
+}  // extern "C"

@@ -1,0 +1,260 @@
+"""fitgpu — MI355X-native batched job→node placement for slurm-bridge-operator.
+
+Python face of libfitgpu.so (C-ABI: include/fitgpu.h).  The names mirror the reference's Go
+functions on the resource-fit path so the tests read like the reference's own:
+
+    ParseDuration                 pkg/slurm-agent/parse.go:36-109
+    parse_resources               parse.go:111-190          (parseResources)
+    parse_nodes                   slurm.go:343-364 + parse.go:291-308 (Client.Nodes/parseNode)
+    parse_partition               parse.go:278-289          (parsePartition)
+    parse_partitions_names        parse.go:192-210          (parsePartitionsNames)
+    extract_batch_resources       pkg/slurm-bridge-operator/parse.go:30-69
+    apply_spec                    pod.go:70-107             (setRequireResourceBySpec + defaults)
+    parse_array_len               parse.go:126-135          (parseArrayLen)
+    gen_resource_list_for_pod     pod.go:143-162            (genResourceListForPod)
+    get_partition_capacity        pkg/slurm-virtual-kubelet/node.go:169-199
+    Engine.place                  the fit decision the reference leaves to kube-scheduler/slurmctld
+
+Every compute call goes through the HIP library; nothing here computes a placement.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import (FIT_E_PARSE, FIT_E_UNLIMITED, FIT_REJECTED, FIT_UNPLACED, FitError, FitJobResources,
+                   FitNode, FitOpts, FitResources, FitStats, check, lib)
+
+__all__ = [
+    "Engine", "FitError", "ErrDurationIsUnlimited", "ParseDuration", "parse_resources", "parse_nodes",
+    "parse_partition", "parse_partitions_names", "extract_batch_resources", "apply_spec",
+    "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
+    "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources",
+]
+
+
+class ErrDurationIsUnlimited(Exception):
+    """pkg/slurm-agent/slurm.go:49 — the duration field has value UNLIMITED (or is empty)."""
+
+
+def _ptr(a) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data) if isinstance(a, np.ndarray) else C.c_void_p(a.data_ptr())
+
+
+# ------------------------------------------------------------------------------- ingest
+def ParseDuration(s: str) -> int:
+    """Duration in nanoseconds; raises ErrDurationIsUnlimited / ValueError like the Go errors."""
+    ns = C.c_int64()
+    rc = lib().fit_parse_duration(s.encode(), C.byref(ns))
+    if rc == FIT_E_UNLIMITED:
+        raise ErrDurationIsUnlimited(s)
+    if rc == FIT_E_PARSE:
+        raise ValueError(f"invalid duration {s!r}")
+    check(rc, "fit_parse_duration")
+    return ns.value
+
+
+@dataclass
+class Resources:  # pkg/slurm-agent/slurm.go:104-110 (Features unused on this path)
+    Nodes: int
+    MemPerNode: int
+    CPUPerNode: int
+    WallTime: int  # ns, -1 = UNLIMITED
+
+
+def parse_resources(text: str) -> Resources:
+    r = FitResources()
+    rc = lib().fit_parse_resources(text.encode(), C.byref(r))
+    if rc == FIT_E_PARSE:
+        raise ValueError("could not parse partition resources")
+    check(rc, "fit_parse_resources")
+    return Resources(r.nodes, r.mem_per_node, r.cpu_per_node, r.wall_ns)
+
+
+@dataclass
+class Node:  # pkg/slurm-agent/slurm.go:113-121
+    Cpus: int
+    Memory: int
+    Gpus: int
+    AlloCpus: int
+    AlloMemory: int
+    AlloGpus: int
+
+
+def parse_nodes(text: str, cap: int | None = None) -> list[Node]:
+    cap = cap if cap is not None else text.count("\n\n") + 2
+    arr = (FitNode * max(cap, 1))()
+    n = check(lib().fit_parse_nodes(text.encode(), arr, cap), "fit_parse_nodes")
+    return [Node(a.cpus, a.memory, a.gpus, a.allo_cpus, a.allo_memory, a.allo_gpus) for a in arr[:n]]
+
+
+def _names(fn, text: str) -> list[str]:
+    buflen = len(text.encode()) * 2 + 64
+    buf = C.create_string_buffer(buflen)
+    n = check(fn(text.encode(), buf, buflen), fn.__name__)
+    return [s.decode() for s in buf.raw.split(b"\0")[:n]]
+
+
+def parse_partition(text: str) -> list[str]:
+    return _names(lib().fit_parse_partition, text)
+
+
+def parse_partitions_names(text: str) -> list[str]:
+    return _names(lib().fit_parse_partitions_names, text)
+
+
+@dataclass
+class JobResources:  # apis/kubecluster.org/v1alpha1/affinity.go:40-48
+    Nodes: int = 0
+    CpusPerTask: int = 0
+    Ntasks: int = 0
+    NtasksPerNode: int = 0
+    MemPerCpu: int = 0
+    WallTime: int = 0
+    Array: str = ""
+
+    def _c(self) -> FitJobResources:
+        r = FitJobResources()
+        r.nodes, r.cpus_per_task, r.ntasks = self.Nodes, self.CpusPerTask, self.Ntasks
+        r.ntasks_per_node, r.mem_per_cpu, r.wall_ns = self.NtasksPerNode, self.MemPerCpu, self.WallTime
+        r.array = self.Array.encode()[:63]
+        return r
+
+    @staticmethod
+    def _py(r: FitJobResources) -> "JobResources":
+        return JobResources(r.nodes, r.cpus_per_task, r.ntasks, r.ntasks_per_node, r.mem_per_cpu,
+                            r.wall_ns, r.array.decode())
+
+
+def extract_batch_resources(script: str) -> JobResources:
+    r = FitJobResources()
+    rc = lib().fit_extract_batch_resources(script.encode(), C.byref(r))
+    if rc == FIT_E_PARSE:
+        raise ValueError("could not extract required resources")
+    check(rc, "fit_extract_batch_resources")
+    return JobResources._py(r)
+
+
+def apply_spec(res: JobResources, nodes=0, cpus_per_task=0, mem_per_cpu=0, ntasks_per_node=0,
+               array="", ntasks=0) -> JobResources:
+    r = res._c()
+    lib().fit_apply_spec(C.byref(r), nodes, cpus_per_task, mem_per_cpu, ntasks_per_node,
+                         array.encode(), ntasks)
+    return JobResources._py(r)
+
+
+def parse_array_len(array: str) -> int:
+    return lib().fit_array_len(array.encode())
+
+
+def gen_resource_list_for_pod(res: JobResources) -> dict:
+    cpu, mem = C.c_int64(), C.c_int64()
+    lib().fit_pod_request(C.byref(res._c()), C.byref(cpu), C.byref(mem))
+    return {"cpu": cpu.value, "memory": mem.value}
+
+
+def job_demand(res: JobResources) -> tuple[int, int, int, int]:
+    """(cpus per node, MiB per node, walltime minutes, nodes) — DESIGN.md §2 demand rule."""
+    cpu, mem, wall, k = C.c_int32(), C.c_int32(), C.c_int32(), C.c_uint16()
+    check(lib().fit_job_demand(C.byref(res._c()), C.byref(cpu), C.byref(mem), C.byref(wall),
+                               C.byref(k)), "fit_job_demand")
+    return cpu.value, mem.value, wall.value, k.value
+
+
+def get_partition_capacity(nodes: list[Node]) -> dict:
+    arr = (FitNode * max(len(nodes), 1))()
+    for i, n in enumerate(nodes):
+        arr[i] = FitNode(n.Cpus, n.Memory, n.Gpus, n.AlloCpus, n.AlloMemory, n.AlloGpus)
+    cpu, mem, gpu, pods = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+    lib().fit_partition_capacity(arr, len(nodes), C.byref(cpu), C.byref(mem), C.byref(gpu), C.byref(pods))
+    out = {"cpu": cpu.value, "memory": mem.value, "pods": pods.value}
+    if gpu.value > 0:
+        out["nvidia.com/gpu"] = gpu.value
+    return out
+
+
+# ------------------------------------------------------------------------------- engine
+def nccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check(lib().fit_nccl_unique_id(buf), "fit_nccl_unique_id")
+    return buf.raw
+
+
+class Engine:
+    """One placement context on one GPU (optionally one rank of a node-sharded group)."""
+
+    def __init__(self, device: int = -1, rank: int = 0, world: int = 1, nccl_id: bytes | None = None,
+                 window_min: int = 0, window_max: int = 0, shard_mode: int = 0):
+        self._idbuf = C.create_string_buffer(nccl_id, 128) if nccl_id else None
+        o = FitOpts(device, rank, world, C.cast(self._idbuf, C.c_void_p) if self._idbuf else None,
+                    shard_mode, window_min, window_max, 0)
+        h = C.c_void_p()
+        check(lib().fit_create(C.byref(o), C.byref(h)), "fit_create")
+        self._h = h
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fit_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def load_nodes(self, nodes):
+        cols = [np.ascontiguousarray(nodes.cpu_free, np.int32), np.ascontiguousarray(nodes.mem_free, np.int32),
+                np.ascontiguousarray(nodes.gpu_free, np.int32), np.ascontiguousarray(nodes.avail_min, np.int32),
+                np.ascontiguousarray(nodes.part_mask, np.uint32)]
+        n = len(cols[0])
+        check(lib().fit_load_nodes(self._h, n, *[_ptr(c) for c in cols]), "fit_load_nodes")
+        self.n = n
+
+    def load_nodes_device(self, cpu, mem, gpu, avail, mask):
+        """torch tensors on this context's GPU (int32 / int32 / int32 / int32 / int32-viewed uint32)."""
+        n = int(cpu.numel())
+        check(lib().fit_load_nodes_device(self._h, n, *[_ptr(t) for t in (cpu, mem, gpu, avail, mask)]),
+              "fit_load_nodes_device")
+        self.n = n
+
+    def load_partitions(self, parts):
+        cols = [np.ascontiguousarray(a, np.int32) for a in (parts.max_time_min, parts.max_cpus_per_node,
+                                                            parts.max_mem_per_node)]
+        check(lib().fit_load_partitions(self._h, len(cols[0]), *[_ptr(c) for c in cols]),
+              "fit_load_partitions")
+
+    def place(self, jobs, kmax: int = 1):
+        cols = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
+        part = np.ascontiguousarray(jobs.part, np.uint16)
+        k = np.ascontiguousarray(jobs.nodes_k, np.uint16)
+        j = len(part)
+        out = np.empty((j, kmax), np.int32)
+        st = FitStats()
+        check(lib().fit_place(self._h, j, *[_ptr(c) for c in cols], _ptr(part), _ptr(k), kmax, _ptr(out),
+                              C.byref(st)), "fit_place")
+        return out, st.as_dict()
+
+    def place_device(self, cpu, mem, gpu, wall, part, nodes_k, out, kmax: int = 1):
+        """All arguments torch tensors resident on this GPU; writes out[J*kmax]."""
+        st = FitStats()
+        check(lib().fit_place_device(self._h, int(cpu.numel()), _ptr(cpu), _ptr(mem), _ptr(gpu), _ptr(wall),
+                                     _ptr(part), _ptr(nodes_k) if nodes_k is not None else None, kmax,
+                                     _ptr(out), C.byref(st)), "fit_place_device")
+        return st.as_dict()
+
+    def read_nodes(self):
+        c, m, g = (np.empty(self.n, np.int32) for _ in range(3))
+        check(lib().fit_read_nodes(self._h, _ptr(c), _ptr(m), _ptr(g)), "fit_read_nodes")
+        return c, m, g
+
+    def partition_free(self, p: int):
+        c, m, g = C.c_int64(), C.c_int64(), C.c_int64()
+        check(lib().fit_partition_free(self._h, p, C.byref(c), C.byref(m), C.byref(g)), "fit_partition_free")
+        return {"cpu": c.value, "mem_mib": m.value, "gpu": g.value}

@@ -1,0 +1,129 @@
+"""ctypes binding of libfitgpu.so (the C-ABI in include/fitgpu.h).
+
+This is the Python twin of the cgo binding shown in INTEGRATION.md; it only marshals pointers.
+Loading fails loudly when the library is missing — there is no fallback implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfitgpu.so")
+
+FIT_OK = 0
+FIT_E_INVAL = -1
+FIT_E_HIP = -2
+FIT_E_RCCL = -3
+FIT_E_OOM = -4
+FIT_E_NODEV = -5
+FIT_E_STATE = -6
+FIT_E_PARSE = -7
+FIT_E_UNLIMITED = -8
+FIT_UNPLACED = -1
+FIT_REJECTED = -2
+
+# every symbol include/fitgpu.h declares (tests/test_abi.py checks the header agrees)
+EXPORTS = [
+    "fit_create", "fit_destroy", "fit_abi_version", "fit_strerror", "fit_last_error",
+    "fit_nccl_unique_id", "fit_load_nodes", "fit_load_nodes_device", "fit_load_partitions",
+    "fit_place", "fit_place_device", "fit_read_nodes", "fit_partition_free",
+    "fit_parse_duration", "fit_parse_resources", "fit_parse_nodes", "fit_parse_partition",
+    "fit_parse_partitions_names", "fit_extract_batch_resources", "fit_apply_spec", "fit_array_len",
+    "fit_pod_request", "fit_job_demand", "fit_partition_capacity",
+]
+
+
+class FitOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32),
+                ("nccl_id", C.c_void_p), ("shard_mode", C.c_int32), ("window_min", C.c_int32),
+                ("window_max", C.c_int32), ("flags", C.c_int32)]
+
+
+class FitStats(C.Structure):
+    _fields_ = [("jobs", C.c_int64), ("placed", C.c_int64), ("unplaced", C.c_int64),
+                ("rejected", C.c_int64), ("rounds", C.c_int64), ("evals", C.c_int64),
+                ("useful_evals", C.c_int64), ("stops_rescan", C.c_int64),
+                ("stops_dirty", C.c_int64), ("ms_total", C.c_double), ("ms_scan", C.c_double),
+                ("ms_commit", C.c_double), ("ms_exchange", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class FitResources(C.Structure):
+    _fields_ = [("nodes", C.c_int64), ("mem_per_node", C.c_int64), ("cpu_per_node", C.c_int64),
+                ("wall_ns", C.c_int64)]
+
+
+class FitNode(C.Structure):
+    _fields_ = [("cpus", C.c_int64), ("memory", C.c_int64), ("gpus", C.c_int64),
+                ("allo_cpus", C.c_int64), ("allo_memory", C.c_int64), ("allo_gpus", C.c_int64)]
+
+
+class FitJobResources(C.Structure):
+    _fields_ = [("nodes", C.c_int64), ("cpus_per_task", C.c_int64), ("ntasks", C.c_int64),
+                ("ntasks_per_node", C.c_int64), ("mem_per_cpu", C.c_int64), ("wall_ns", C.c_int64),
+                ("array", C.c_char * 64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libfitgpu.so (built by __graft_entry__.build() / `make`); raise if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C slurm-bridge-operator_amd`")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        i32, i64, u16p = C.c_int32, C.c_int64, C.POINTER(C.c_uint16)
+        L.fit_strerror.restype = C.c_char_p
+        L.fit_strerror.argtypes = [C.c_int]
+        L.fit_last_error.restype = C.c_char_p
+        L.fit_create.argtypes = [C.POINTER(FitOpts), C.POINTER(P)]
+        L.fit_destroy.argtypes = [P]
+        L.fit_destroy.restype = None
+        L.fit_nccl_unique_id.argtypes = [P]
+        for name in ("fit_load_nodes", "fit_load_nodes_device"):
+            getattr(L, name).argtypes = [P, i32, P, P, P, P, P]
+        L.fit_load_partitions.argtypes = [P, i32, P, P, P]
+        for name in ("fit_place", "fit_place_device"):
+            getattr(L, name).argtypes = [P, i32, P, P, P, P, P, P, i32, P, C.POINTER(FitStats)]
+        L.fit_read_nodes.argtypes = [P, P, P, P]
+        L.fit_partition_free.argtypes = [P, i32, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
+        L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
+        L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]
+        L.fit_parse_nodes.argtypes = [C.c_char_p, C.POINTER(FitNode), i32]
+        L.fit_parse_partition.argtypes = [C.c_char_p, C.c_char_p, i32]
+        L.fit_parse_partitions_names.argtypes = [C.c_char_p, C.c_char_p, i32]
+        L.fit_extract_batch_resources.argtypes = [C.c_char_p, C.POINTER(FitJobResources)]
+        L.fit_apply_spec.argtypes = [C.POINTER(FitJobResources), i64, i64, i64, i64, C.c_char_p, i64]
+        L.fit_apply_spec.restype = None
+        L.fit_array_len.argtypes = [C.c_char_p]
+        L.fit_array_len.restype = i64
+        L.fit_pod_request.argtypes = [C.POINTER(FitJobResources), C.POINTER(i64), C.POINTER(i64)]
+        L.fit_pod_request.restype = None
+        L.fit_job_demand.argtypes = [C.POINTER(FitJobResources), C.POINTER(i32), C.POINTER(i32),
+                                     C.POINTER(i32), u16p]
+        L.fit_partition_capacity.argtypes = [C.POINTER(FitNode), i32, C.POINTER(i64),
+                                             C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
+        L.fit_partition_capacity.restype = None
+        _lib = L
+    return _lib
+
+
+class FitError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        L = lib()
+        msg = L.fit_strerror(code).decode()
+        detail = (L.fit_last_error() or b"").decode()
+        super().__init__(f"{where}: {msg} ({code}): {detail}")
+        self.code = code
+
+
+def check(rc: int, where: str) -> int:
+    if rc < 0:
+        raise FitError(rc, where)
+    return rc
