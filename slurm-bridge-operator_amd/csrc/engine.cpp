@@ -25,7 +25,7 @@ hipError_t launch_scan(int blocks, hipStream_t st, const NodeRec* rec, const int
                        const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
                        const CompPlan* plan, int ncomp, uint64_t* cand, uint64_t* bnd,
                        JobRec* wjob);
-hipError_t launch_commit(int ncomp, size_t lds_bytes, hipStream_t st, NodeRec* rec,
+hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, NodeRec* rec,
                          const CompPlan* plan, const uint64_t* cand, int64_t rank_stride,
                          int nranks, const uint64_t* bnd, const JobRec* wjob, int32_t* out,
                          int kmax, CommitResult* res);
@@ -312,6 +312,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     float ms;
     for (;;) {
         int64_t blocks = 0, slots = 0, cand_n = 0, evals = 0;
+        int epl = 1;
         size_t lds = 0;
         bool any = false;
         for (int k = 0; k < C; ++k) {
@@ -323,7 +324,10 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             const int32_t per = (len + c->world - 1) / c->world;
             P.sb = std::min(P.ne, P.nb + per * c->rank);
             P.se = std::min(P.ne, P.sb + per);
-            P.nslice = std::max(1, (per + SLICE - 1) / SLICE);
+            // sub-slices of >= MIN_SUB nodes, at most MAX_SLICES block-slices per job per rank
+            P.sub = std::max(MIN_SUB, (per + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
+            P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
+            epl = std::max(epl, (c->world * P.nslice * KS + 63) / 64);
             P.jbase = cur[k];
             P.w = std::min(win[k], jb[k + 1] - cur[k]);
             P.blk0 = (int32_t)blocks;
@@ -331,7 +335,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             P.slot0 = (int32_t)slots;
             if (P.w > 0) {
                 any = true;
-                blocks += (int64_t)((P.w + SCAN_BLOCK - 1) / SCAN_BLOCK) * P.nslice;
+                blocks += (int64_t)((P.w + SCAN_JOBS - 1) / SCAN_JOBS) * P.nslice;
                 cand_n += (int64_t)P.w * P.nslice * KS;
                 slots += P.w;
                 evals += (int64_t)P.w * (P.se - P.sb);
@@ -359,7 +363,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             NCCL_TRY(ncclAllReduce(c->bnd.p, c->bnd.p, slots, ncclUint64, ncclMin, c->comm, st));
         }
         HIP_TRY(hipEventRecord(c->ev[2], st));
-        HIP_TRY(launch_commit(C, lds, st, c->rec.p, c->plan.p, c->cand.p, cand_n, c->world,
+        HIP_TRY(launch_commit(C, epl, lds, st, c->rec.p, c->plan.p, c->cand.p, cand_n, c->world,
                               c->bnd.p, c->wjob.p, out, kmax, c->res.p));
         HIP_TRY(hipEventRecord(c->ev[3], st));
         HIP_TRY(hipMemcpyAsync(c->h_res.p, c->res.p, sizeof(CommitResult) * C,

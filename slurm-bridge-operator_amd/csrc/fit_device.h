@@ -4,10 +4,12 @@
 
 namespace fitgpu {
 
-constexpr int KS = 16;          // candidates kept per (job, node slice) by fit_scan
-constexpr int SLICE = 2048;     // nodes per scan slice (one scan block walks one slice)
+constexpr int KS = 16;          // candidates kept per (job, block-slice) by fit_scan
+constexpr int SCAN_WAVES = 8;   // waves per scan block; each walks one sub-slice of nodes
+constexpr int SCAN_JOBS = 64;   // jobs per scan block (lanes = jobs, shared by the 8 waves)
+constexpr int MIN_SUB = 256;    // minimum nodes per wave sub-slice
+constexpr int MAX_SLICES = 4;   // block-slices per job per rank (sub-slice grows past this)
 constexpr int UCAP = 256;       // dirty-node capacity per component per round (4 per lane)
-constexpr int SCAN_BLOCK = 256; // jobs per scan block (4 waves, lanes = jobs)
 constexpr int MAX_COMPONENT_NODES = 1 << 20;  // LDS dirty bitmap limit (128 KiB)
 constexpr uint64_t KEY_INF = ~0ull;
 
@@ -32,13 +34,13 @@ struct alignas(32) JobRec {
 struct alignas(16) CompPlan {
     int32_t nb, ne;      // component's node positions [nb, ne)
     int32_t sb, se;      // this rank's scan range inside it
-    int32_t nslice;      // slices per job on every rank
+    int32_t nslice;      // block-slices per job on every rank (<= MAX_SLICES)
+    int32_t sub;         // nodes per wave sub-slice (block-slice = SCAN_WAVES * sub)
     int32_t jbase;       // first window job's index into the component job list
     int32_t w;           // window size (jobs)
     int32_t blk0;        // first fit_scan block of this component
     int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
     int32_t slot0;       // first window slot (global over components)
-    int32_t pad;
 };
 
 struct CommitResult {

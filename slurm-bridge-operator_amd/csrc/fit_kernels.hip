@@ -11,6 +11,8 @@
 // The sequential semantics they reproduce bit-exactly is oracle/fitref.c:ref_place.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fit_device.h"
 
 namespace fitgpu {
@@ -24,38 +26,72 @@ __device__ __forceinline__ uint64_t fit_key(int32_t cf, int32_t mf, int32_t gf, 
     return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
 }
 
-// ---- wave-wide 64-bit min over all 64 lanes (DPP; call with a full EXEC mask) ----------
+// ---- wave-wide reductions (DPP; call with a full EXEC mask) ---------------------------
 template <int CTRL, int ROWMASK>
-__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
-    uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(uint32_t)v, CTRL,
-                                                        ROWMASK, 0xf, false);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(uint32_t)(v >> 32),
-                                                        CTRL, ROWMASK, 0xf, false);
-    return ((uint64_t)hi << 32) | lo;
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, CTRL, ROWMASK,
+                                                        0xf, false));
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_min<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_min<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_min<0x124, 0xf>(v);  // row_ror:4
+    v = dpp_min<0x128, 0xf>(v);  // row_ror:8
+    v = dpp_min<0x142, 0xa>(v);  // row_bcast:15
+    v = dpp_min<0x143, 0xc>(v);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// min over the wave of a packed (score << 32 | position) key: 32-bit min of the scores, then of
+// the positions among the lanes holding that score (usually one lane: a readlane).
+__device__ __forceinline__ uint64_t wave_min_key(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t mh = wave_min_u32(hi);
+    const uint64_t eq = __ballot(hi == mh);
+    uint32_t ml;
+    if (__popcll(eq) == 1)
+        ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(eq));
+    else
+        ml = wave_min_u32(hi == mh ? lo : 0xffffffffu);
+    return ((uint64_t)mh << 32) | ml;
 }
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
-
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-    v = umin64(v, dpp64<0xb1, 0xf>(v));   // quad_perm [1,0,3,2]
-    v = umin64(v, dpp64<0x4e, 0xf>(v));   // quad_perm [2,3,0,1]
-    v = umin64(v, dpp64<0x124, 0xf>(v));  // row_ror:4
-    v = umin64(v, dpp64<0x128, 0xf>(v));  // row_ror:8
-    v = umin64(v, dpp64<0x142, 0xa>(v));  // row_bcast:15
-    v = umin64(v, dpp64<0x143, 0xc>(v));  // row_bcast:31
-    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
-    return ((uint64_t)hi << 32) | lo;
-}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
 
 // sorted ascending insert of x into key[0..KS) dropping the largest (static indices only)
 __device__ __forceinline__ void topk_insert(uint64_t (&key)[KS], uint64_t x) {
 #pragma unroll
-    for (int i = KS - 1; i > 0; --i) {
-        uint64_t a = key[i - 1], b = key[i];
-        key[i] = a > x ? a : (b > x ? x : b);
+    for (int i = KS - 1; i > 0; --i) key[i] = umax64(key[i - 1], umin64(key[i], x));
+    key[0] = umin64(key[0], x);
+}
+
+// (list, bound) pairs: every node of the covered range that is not in the sorted list has a
+// key > bound, and every list entry is <= bound (bound = last entry, INF when not full).
+// Merge two such pairs over disjoint ranges into the pair for the union (bitonic, registers).
+__device__ __forceinline__ void merge_lists(uint64_t (&a)[KS], const uint64_t (&b)[KS]) {
+    const uint64_t bb = umin64(a[KS - 1], b[KS - 1]);
+    uint64_t c[KS];
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const uint64_t x = a[i] > bb ? KEY_INF : a[i];
+        const uint64_t y = b[KS - 1 - i] > bb ? KEY_INF : b[KS - 1 - i];
+        c[i] = umin64(x, y);  // bitonic sequence holding the KS smallest of the union
     }
-    key[0] = key[0] > x ? x : key[0];
+#pragma unroll
+    for (int st = KS / 2; st >= 1; st >>= 1)
+#pragma unroll
+        for (int i = 0; i < KS; ++i)
+            if ((i & st) == 0) {
+                const uint64_t lo = umin64(c[i], c[i + st]), hi = umax64(c[i], c[i + st]);
+                c[i] = lo;
+                c[i + st] = hi;
+            }
+#pragma unroll
+    for (int i = 0; i < KS; ++i) a[i] = c[i];
+    // The bound stays "last entry": if bb is finite, the list achieving it is full with all its
+    // KS entries <= bb, so the merged list is full and c[KS-1] <= bb is the new bound.
 }
 
 __device__ __forceinline__ int find_comp(const CompPlan* __restrict__ plan, int ncomp, int b) {
@@ -64,7 +100,6 @@ __device__ __forceinline__ int find_comp(const CompPlan* __restrict__ plan, int 
         if (plan[i].blk0 <= b) c = i;
     return c;
 }
-
 
 // One (job-lane, node-row) evaluation.  Node fields are clamped to >= -1 when the table is built
 // (k_gather_nodes) and demands are >= 0, so every difference below is exact in int32; the pair
@@ -85,25 +120,27 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
 }
 
 // -------------------------------------------------------------------------------- k_scan
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan(
+// Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices (one per wave).
+// Each wave keeps the exact top-KS of its sub-slice; the 8 lists are merged through LDS in a
+// bitonic tree, giving the exact top-KS (and bound) of the block-slice.
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan(
     const NodeRec* __restrict__ rec, const int32_t* __restrict__ jl,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk,
     const CompPlan* __restrict__ plan, int ncomp, uint64_t* __restrict__ cand,
     uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob) {
+    __shared__ uint64_t xk[SCAN_WAVES / 2][KS][64];  // lane-contiguous: conflict-free b64 access
     const int c = find_comp(plan, ncomp, blockIdx.x);
     const CompPlan P = plan[c];
     const int local = blockIdx.x - P.blk0;
     // integer division expands to VALU code: pin the (uniform) results to SGPRs
     const int tile = __builtin_amdgcn_readfirstlane(local / P.nslice);
     const int s = __builtin_amdgcn_readfirstlane(local - tile * P.nslice);
-    const int t = tile * SCAN_BLOCK + threadIdx.x;
-    // wave-uniform by construction; readfirstlane tells the compiler so (keeps the node loop
-    // counter and row addresses in SGPRs)
-    const int wave_first =
-        __builtin_amdgcn_readfirstlane(tile * SCAN_BLOCK + (int)(threadIdx.x & ~63u));
-    if (wave_first >= P.w) return;  // whole wave outside the window
+    if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int t = tile * SCAN_JOBS + lane;
     const bool active = t < P.w;
 
     JobRec J;
@@ -123,12 +160,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(
     // score never beats the K-th entry (positions only grow); a spurious insert when the K-th
     // score is 0 is dropped by the 64-bit insertion network, so the list stays exact.
     uint32_t lim = 0xffffffffu;
-
-    const int n0 = P.sb + s * SLICE;
-    const int n1 = min(P.se, n0 + SLICE);
+    const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
+    const int n1 = min(P.se, n0 + P.sub);
     int x = n0;
-    // 4 rows per batch: four s_load_dwordx8 in flight per wait
-    for (; x + 4 <= n1; x += 4) {
+    for (; x + 4 <= n1; x += 4) {  // 4 rows per batch: four scalar row loads per wait
         NodeRec r[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) r[u] = rec[x + u];
@@ -136,8 +171,24 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(
         for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
     }
     for (; x < n1; ++x) scan_row(rec[x], x, J, key, lim);
-    const bool full = key[KS - 1] != KEY_INF;
-    if (!active) return;
+
+    // merge tree: waves [h, 2h) hand their lists to waves [0, h)
+#pragma unroll
+    for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
+        if (wave >= h && wave < 2 * h) {
+#pragma unroll
+            for (int i = 0; i < KS; ++i) xk[wave - h][i][lane] = key[i];
+        }
+        __syncthreads();
+        if (wave < h) {
+            uint64_t o[KS];
+#pragma unroll
+            for (int i = 0; i < KS; ++i) o[i] = xk[wave][i][lane];
+            merge_lists(key, o);
+        }
+        __syncthreads();
+    }
+    if (wave != 0 || !active) return;
     uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KS;
 #pragma unroll
     for (int i = 0; i < KS; i += 2) {
@@ -146,15 +197,172 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan(
         v.y = key[i + 1];
         *reinterpret_cast<ulonglong2*>(dst + i) = v;
     }
-    // every node outside this slice's list has a key > key[KS-1] (list full) — bound B
-    if (full) atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
-                        (unsigned long long)key[KS - 1]);
+    if (key[KS - 1] != KEY_INF)
+        atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
+                  (unsigned long long)key[KS - 1]);
     if (s == 0) wjob[P.slot0 + t] = J;
 }
-
 // ------------------------------------------------------------------------------ k_commit
+// One wave per component walks the window in priority order.  For job t it needs
+//   clean best  = min over its candidate entries <= B whose node is not dirty (LDS bitmap),
+//   dirty best  = min over the dirty rows (held in VGPRs, UPL per lane) at their current state,
+// then commits min(clean, dirty) or stops the round.  The candidate keys, job
+// row and bound are loaded two jobs ahead and the candidates' node rows one job ahead, so the
+// serial chain per job is LDS + VALU + one wave reduction.
 constexpr int UPL = UCAP / 64;  // dirty slots per lane
 
+// ---- diagnostic in-kernel stamps (only in the FIT_STAMPS build; never in the shipped kernel)
+#ifdef FIT_STAMPS
+__device__ unsigned long long g_stamps[64][8];
+#define STAMP_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long st_prev = 0; \
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+#define STAMP(i)                                                                          \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        unsigned long long now_;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");      \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        if (i > 0) st_acc[(i) > 0 ? (i) - 1 : 0] += now_ - st_prev;                                     \
+        st_prev = now_;                                                                   \
+    } while (0)
+#define STAMP_FLUSH(c, n)                                                                 \
+    {                                                                                     \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                      \
+        const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime();                  \
+        if (threadIdx.x == 0) {                                                           \
+            for (int i_ = 0; i_ < 6; ++i_) g_stamps[c][i_] = st_acc[i_];                  \
+            g_stamps[c][6] = n;                                                           \
+            g_stamps[c][7] = ((t1_ - st_t0) << 24) / max(r1_ - st_r0, 1ull); /* cyc/10ns << 24 */ \
+        }                                                                                 \
+    }
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH(c, n)
+#endif
+
+struct CRow {  // node row of a candidate (prefetched)
+    int32_t cpu, mem, gpu, avail;
+    uint32_t mask;
+    int32_t orig;
+};
+
+// Pipeline.  Iteration t: vector-load the keys of job t+2; derive the clean
+// flags of job t+1 (bound + dirty bitmap, before job t's commit); resolve job t; clear the flag
+// of any job-(t+1) candidate equal to the node job t dirtied; scalar-load job t+3's row and
+// bound.  Every wait is then on data requested at least one iteration earlier.  The 4-slot
+// job ring is indexed by literal constants only (4-way unrolled loop) so it stays in registers.
+#define FIT_COMMIT_STEP(A, N1, N2, N3)                                                            \
+    {                                                                                           \
+        if (t >= P.w) goto done;                                                                \
+        STAMP(0);                                                                               \
+        {                                                                                       \
+            const int tc_ = min(t + 2, wlast);                                                  \
+            _Pragma("unroll") for (int k = 0; k < EPL; ++k) kr[N2][k] =                         \
+                cand[off[k] + (int64_t)tc_ * per_rank];                                         \
+        }                                                                                       \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) {                                       \
+            const uint64_t kk_ = kr[N1][k];                                                     \
+            const bool v_ = has[k] && kk_ <= jb[N1] && kk_ != KEY_INF;                          \
+            const uint32_t rel_ = v_ ? (uint32_t)kk_ - nb : 0u;                                 \
+            cl[N1][k] = v_ && !((bitmap[rel_ >> 5] >> (rel_ & 31)) & 1u);                       \
+        }                                                                                       \
+        STAMP(1);                                                                               \
+        const int32_t jc = jcr[A], jm = jmr[A], jg = jgr[A], jw = jwr[A];                       \
+        const uint32_t jp = jpr[A];                                                             \
+        const uint64_t B = jb[A];                                                               \
+        uint64_t cm = KEY_INF;                                                                  \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) cm =                                    \
+            umin64(cm, cl[A][k] ? kr[A][k] : KEY_INF);                                          \
+        STAMP(2);                                                                               \
+        uint64_t dk[UPL];                                                                       \
+        uint64_t dm = KEY_INF;                                                                  \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) {                                       \
+            dk[i] = KEY_INF;                                                                    \
+            if (i * 64 < nu) {                                                                  \
+                const int32_t dc = ucpu[i] - jc, dmm = umem[i] - jm;                            \
+                const int32_t dg = ugpu[i] - jg, da = uav[i] - jw;                              \
+                const bool ok = (dc | dmm | dg | da) >= 0 && (umask[i] & jp) &&                 \
+                                i * 64 + lane < nu;                                             \
+                const uint32_t sc = (min((uint32_t)dg, 255u) << 24) |                           \
+                                    (min((uint32_t)dc, 4095u) << 12) |                          \
+                                    min((uint32_t)dmm >> 10, 4095u);                            \
+                dk[i] = ok ? (((uint64_t)sc << 32) | upos[i]) : KEY_INF;                        \
+                dm = umin64(dm, dk[i]);                                                         \
+            }                                                                                   \
+        }                                                                                       \
+        STAMP(3);                                                                               \
+        const uint64_t best = wave_min_key(umin64(cm, dm));                                     \
+        STAMP(4);                                                                               \
+        if (B != KEY_INF && best > B && __ballot(cm != KEY_INF) == 0ull) {                      \
+            stop = 1; /* candidate list exhausted: rescan next round */                         \
+            goto done;                                                                          \
+        }                                                                                       \
+        int32_t node = -1;                                                                      \
+        uint32_t newpos = 0xffffffffu;                                                          \
+        if (best != KEY_INF) {                                                                  \
+            const uint64_t dmask = __ballot(dm == best);                                        \
+            if (dmask) { /* a dirty row wins: update it in place */                             \
+                int32_t o = 0;                                                                  \
+                _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {              \
+                    const bool hit_ = dk[i] == best;                                            \
+                    ucpu[i] -= hit_ ? jc : 0;                                                   \
+                    umem[i] -= hit_ ? jm : 0;                                                   \
+                    ugpu[i] -= hit_ ? jg : 0;                                                   \
+                    o = hit_ ? uorig[i] : o;                                                    \
+                }                                                                               \
+                node = __builtin_amdgcn_readlane(o, __builtin_ctzll(dmask));                    \
+            } else { /* a clean candidate wins: its row becomes dirty row nu */                 \
+                if (nu == UCAP) {                                                               \
+                    stop = 2;                                                                   \
+                    goto done;                                                                  \
+                }                                                                               \
+                newpos = (uint32_t)best;                                                        \
+                const NodeRec r = rec[newpos];                                                  \
+                node = r.orig;                                                                  \
+                if (lane == (nu & 63)) {                                                        \
+                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i == (nu >> 6)) {       \
+                        ucpu[i] = r.cpu - jc;                                                   \
+                        umem[i] = r.mem - jm;                                                   \
+                        ugpu[i] = r.gpu - jg;                                                   \
+                        uav[i] = r.avail;                                                       \
+                        umask[i] = r.mask;                                                      \
+                        upos[i] = newpos;                                                       \
+                        uorig[i] = node;                                                        \
+                    }                                                                           \
+                    const uint32_t rel = newpos - nb;                                           \
+                    bitmap[rel >> 5] |= 1u << (rel & 31);                                       \
+                }                                                                               \
+                ++nu;                                                                           \
+            }                                                                                   \
+            ++placed;                                                                           \
+        }                                                                                       \
+        STAMP(5);                                                                               \
+        if (lane == (t & 63)) {                                                                 \
+            oq = jqr[A];                                                                        \
+            ov = node;                                                                          \
+        }                                                                                       \
+        if ((t & 63) == 63) { /* uniform: flush 64 placements */                                \
+            if (oq >= 0) out[(int64_t)oq * kmax] = ov;                                          \
+            oq = -1;                                                                            \
+        }                                                                                       \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) cl[N1][k] =                             \
+            cl[N1][k] && (uint32_t)kr[N1][k] != newpos;                                         \
+        {                                                                                       \
+            const int tc_ = min(t + 3, wlast); /* slot N3 (job t-1's) receives job t+3 */       \
+            const JobRec J_ = wjob[P.slot0 + tc_];                                              \
+            jqr[N3] = J_.q;                                                                     \
+            jcr[N3] = J_.cpu;                                                                   \
+            jmr[N3] = J_.mem;                                                                   \
+            jgr[N3] = J_.gpu;                                                                   \
+            jwr[N3] = J_.wall;                                                                  \
+            jpr[N3] = J_.pbit;                                                                  \
+            jb[N3] = bnd[P.slot0 + tc_];                                                        \
+        }                                                                                       \
+        ++t;                                                                                    \
+    }
+
+template <int EPL>
 __global__ __launch_bounds__(64) void k_commit(
     NodeRec* __restrict__ rec, const CompPlan* __restrict__ plan,
     const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
@@ -172,89 +380,67 @@ __global__ __launch_bounds__(64) void k_commit(
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
     __syncthreads();
 
+    const int per_rank = P.nslice * KS;
+    const int E = nranks * per_rank;
+    int64_t off[EPL];
+    bool has[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int e = lane + 64 * k;
+        const int g = e / per_rank;
+        has[k] = e < E;
+        off[k] = has[k] ? g * rank_stride + P.cand_off + (e - g * per_rank) : P.cand_off;
+    }
+    const int wlast = P.w - 1;
+    const uint32_t nb = (uint32_t)P.nb;
+
     int32_t ucpu[UPL], umem[UPL], ugpu[UPL], uav[UPL], uorig[UPL];
     uint32_t umask[UPL], upos[UPL];
 #pragma unroll
     for (int i = 0; i < UPL; ++i) {
         ucpu[i] = umem[i] = ugpu[i] = uav[i] = uorig[i] = 0;
-        umask[i] = 0u;
-        upos[i] = 0u;
+        umask[i] = upos[i] = 0u;
     }
     int nu = 0, placed = 0, stop = 0, t = 0;
-    const int per_rank = P.nslice * KS;
-    const int E = nranks * per_rank;
+    int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
 
-    for (; t < P.w; ++t) {
-        const JobRec J = wjob[P.slot0 + t];
-        const uint64_t B = bnd[P.slot0 + t];
-        // best clean candidate held by this lane
-        uint64_t cm = KEY_INF;
-        for (int e = lane; e < E; e += 64) {
-            const int g = e / per_rank;
-            const int r = e - g * per_rank;
-            const uint64_t k = cand[g * rank_stride + P.cand_off + (int64_t)t * per_rank + r];
-            if (k != KEY_INF && k <= B) {
-                const uint32_t rel = (uint32_t)k - (uint32_t)P.nb;
-                const bool dirty = (bitmap[rel >> 5] >> (rel & 31)) & 1u;
-                if (!dirty) cm = umin64(cm, k);
-            }
-        }
-        // current keys of the dirty rows held by this lane
-        uint64_t dk[UPL];
-        uint64_t dm = KEY_INF;
+    uint64_t kr[4][EPL];
+    bool cl[4][EPL];
+    int32_t jqr[4], jcr[4], jmr[4], jgr[4], jwr[4];
+    uint32_t jpr[4];
+    uint64_t jb[4];
 #pragma unroll
-        for (int i = 0; i < UPL; ++i) {
-            dk[i] = (i * 64 + lane < nu)
-                        ? fit_key(ucpu[i], umem[i], ugpu[i], uav[i], umask[i], upos[i], J)
-                        : KEY_INF;
-            dm = umin64(dm, dk[i]);
-        }
-        const uint64_t best = wave_min_u64(umin64(cm, dm));
-        const bool any_clean = __ballot(cm != KEY_INF) != 0ull;
-        if (!any_clean && B != KEY_INF && best > B) {  // list exhausted: rescan next round
-            stop = 1;
-            break;
-        }
-        if (best == KEY_INF) continue;  // FIT_UNPLACED (out pre-set to -1)
-        const uint64_t from_dirty = __ballot(dm == best);
-        if (from_dirty) {
+    for (int s = 0; s < 3; ++s) {
+        const int tc = min(s, wlast);
+        if (s < 2) {
 #pragma unroll
-            for (int i = 0; i < UPL; ++i)
-                if (dk[i] == best) {
-                    ucpu[i] -= J.cpu;
-                    umem[i] -= J.mem;
-                    ugpu[i] -= J.gpu;
-                    out[(int64_t)J.q * kmax] = uorig[i];
-                }
-        } else {
-            if (nu == UCAP) {
-                stop = 2;
-                break;
-            }
-            const uint32_t pos = (uint32_t)best;
-            const int owner = nu & 63, slot = nu >> 6;
-            if (lane == owner) {
-                const NodeRec r = rec[pos];
-#pragma unroll
-                for (int i = 0; i < UPL; ++i)
-                    if (i == slot) {
-                        ucpu[i] = r.cpu - J.cpu;
-                        umem[i] = r.mem - J.mem;
-                        ugpu[i] = r.gpu - J.gpu;
-                        uav[i] = r.avail;
-                        umask[i] = r.mask;
-                        upos[i] = pos;
-                        uorig[i] = r.orig;
-                    }
-                out[(int64_t)J.q * kmax] = r.orig;
-                const uint32_t rel = pos - (uint32_t)P.nb;
-                bitmap[rel >> 5] |= 1u << (rel & 31);
-            }
-            ++nu;
-            __syncthreads();  // bitmap write visible to the next job's lookups
+            for (int k = 0; k < EPL; ++k) kr[s][k] = cand[off[k] + (int64_t)tc * per_rank];
         }
-        ++placed;
+        const JobRec J = wjob[P.slot0 + tc];
+        jqr[s] = J.q;
+        jcr[s] = J.cpu;
+        jmr[s] = J.mem;
+        jgr[s] = J.gpu;
+        jwr[s] = J.wall;
+        jpr[s] = J.pbit;
+        jb[s] = bnd[P.slot0 + tc];
     }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const bool v = has[k] && kr[0][k] <= jb[0] && kr[0][k] != KEY_INF;
+        const uint32_t rel = v ? (uint32_t)kr[0][k] - nb : 0u;
+        cl[0][k] = v && !((bitmap[rel >> 5] >> (rel & 31)) & 1u);
+    }
+    STAMP_DECL
+    for (;;) {
+        FIT_COMMIT_STEP(0, 1, 2, 3)
+        FIT_COMMIT_STEP(1, 2, 3, 0)
+        FIT_COMMIT_STEP(2, 3, 0, 1)
+        FIT_COMMIT_STEP(3, 0, 1, 2)
+    }
+done:
+    STAMP_FLUSH(c, t)
+    if (oq >= 0 && (lane < (t & 63))) out[(int64_t)oq * kmax] = ov;  // last partial group
     // write the dirty rows back for the next round's scan
 #pragma unroll
     for (int i = 0; i < UPL; ++i)
@@ -266,6 +452,7 @@ __global__ __launch_bounds__(64) void k_commit(
         }
     if (lane == 0) res[c] = CommitResult{t, stop, nu, placed};
 }
+#undef FIT_COMMIT_STEP
 
 // ------------------------------------------------------------------- prefilter / setup
 // out[] init, component id per job, rejected marks (FIT_REJECTED) — DESIGN.md §3.1.
@@ -329,19 +516,32 @@ hipError_t launch_scan(int blocks, hipStream_t st, const NodeRec* rec, const int
                        const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
                        const CompPlan* plan, int ncomp, uint64_t* cand, uint64_t* bnd,
                        JobRec* wjob) {
-    hipLaunchKernelGGL(k_scan, dim3(blocks), dim3(SCAN_BLOCK), 0, st, rec, jl, jcpu, jmem, jgpu,
+    hipLaunchKernelGGL(k_scan, dim3(blocks), dim3(SCAN_WAVES * 64), 0, st, rec, jl, jcpu, jmem, jgpu,
                        jwall, jpart, jk, plan, ncomp, cand, bnd, wjob);
     return hipGetLastError();
 }
 
-hipError_t launch_commit(int ncomp, size_t lds_bytes, hipStream_t st, NodeRec* rec,
+hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, NodeRec* rec,
                          const CompPlan* plan, const uint64_t* cand, int64_t rank_stride,
                          int nranks, const uint64_t* bnd, const JobRec* wjob, int32_t* out,
                          int kmax, CommitResult* res) {
-    hipLaunchKernelGGL(k_commit, dim3(ncomp), dim3(64), lds_bytes, st, rec, plan, cand,
-                       rank_stride, nranks, bnd, wjob, out, kmax, res);
+#define FIT_COMMIT(EPL)                                                                      \
+    hipLaunchKernelGGL(k_commit<EPL>, dim3(ncomp), dim3(64), lds_bytes, st, rec, plan, cand, \
+                       rank_stride, nranks, bnd, wjob, out, kmax, res)
+    if (epl <= 1) FIT_COMMIT(1);
+    else if (epl <= 2) FIT_COMMIT(2);
+    else if (epl <= 4) FIT_COMMIT(4);
+    else if (epl <= 8) FIT_COMMIT(8);
+    else return hipErrorInvalidValue;
+#undef FIT_COMMIT
     return hipGetLastError();
 }
+
+#ifdef FIT_STAMPS
+extern "C" int fit_debug_commit_stamps(unsigned long long* out /* 64 x 8 */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* jmem,
                             const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
