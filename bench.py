@@ -45,6 +45,8 @@ def parse_args():
     ap.add_argument("--cpu-sample", type=int, default=40000, help="jobs in the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=None, help="profiles/*_pmc.json with measured HBM bytes/launch")
+    ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
+                    help="N>1 split: auto = partition components when there are >= N of them")
     return ap.parse_args()
 
 
@@ -53,7 +55,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fitgpu import Engine, nccl_unique_id, synth
+    from fitgpu import (FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, Engine, nccl_unique_id,
+                        synth)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -80,7 +83,8 @@ def main():
               T(jobs.nodes_k.view(np.int16))]
     d_out = torch.empty(jobs.j, dtype=torch.int32, device=dev)
 
-    eng = Engine(device=local, rank=rank, world=world, nccl_id=nid)
+    mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
+    eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
     eng.load_partitions(parts)
 
     def step():
@@ -112,13 +116,20 @@ def main():
     value = jobs.j * a.steps / el
     agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan",
                                                   "ms_commit", "ms_exchange", "placed", "unplaced")}
+    evals_local = agg["evals"]
+    if world > 1:  # performed evaluations summed over ranks (each rank scanned its own share)
+        t = torch.tensor([float(agg["evals"])], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        agg["evals"] = int(t.item())
+    used_mode = {0: "1 GPU", 1: f"node-sharded x{world} (RCCL allgather + u64 min-allreduce per round)",
+                 2: f"partition-component-sharded x{world} (one RCCL merge)"}[stats[-1]["shard_mode"]]
     rounds = max(agg["rounds"], 1)
     scan_ms = agg["ms_scan"] / rounds
     commit_ms = agg["ms_commit"] / rounds
-    evals_per_launch = agg["evals"] / rounds
+    evals_per_launch = evals_local / rounds
     scan_tops = evals_per_launch * SCAN_OPS_PER_EVAL / (scan_ms * 1e-3) / 1e12
     # commit: one launch per round resolves (placed+unplaced in window) jobs; bytes model DESIGN §5
-    entries = 64 * world
+    entries = 64 * (world if stats[-1]["shard_mode"] == 1 else 1)
     commit_jobs = (agg["placed"] + agg["unplaced"]) / rounds
     commit_gbs = commit_jobs * commit_bytes_per_job(entries) / (commit_ms * 1e-3) / 1e9
     kernels = {
@@ -159,7 +170,7 @@ def main():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic (splitmix64 generator, fitgpu/synth.py; DESIGN.md §5)",
         "config": {"workload": a.workload, "nodes": nodes.n, "jobs": jobs.j, "partitions": parts.p,
-                   "parallelism": f"node-sharded x{world}" if world > 1 else "1 GPU"},
+                   "parallelism": used_mode, "components": stats[-1]["components"]},
         "fit_evals_per_s": {"useful": round(agg["useful_evals"] / el, 1), "performed": round(agg["evals"] / el, 1)},
         "rounds_per_step": agg["rounds"] / a.steps,
         "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,

@@ -49,17 +49,32 @@ extern "C" {
 
 typedef struct fit_ctx fit_ctx;
 
+/* Optional host-side exchange used instead of RCCL (world > 1): tests run several ranks on one
+ * GPU with it, a caller may route the exchange through its own transport.  In-place on host
+ * memory; return 0 on success.  ops: */
+#define FIT_XCHG_ALLGATHER_U64 1  /* buf holds world*count u64, this rank's block at rank*count */
+#define FIT_XCHG_MIN_U64 2        /* elementwise min over ranks, count u64                    */
+#define FIT_XCHG_MAX_I32 3        /* elementwise max over ranks, count int32                  */
+#define FIT_XCHG_MIN_I32 4        /* elementwise min over ranks, count int32                  */
+typedef int (*fit_exchange_fn)(void* user, int op, void* buf, int64_t count);
+
 typedef struct {
     int32_t device;       /* HIP device ordinal; -1 = current device                        */
     int32_t rank;         /* this process' rank in a node-sharded group (0 if world == 1)  */
     int32_t world;        /* number of GPUs sharing one placement (1 = single GPU)         */
     const void* nccl_id;  /* 128-byte ncclUniqueId from fit_nccl_unique_id() when world>1 */
-    int32_t shard_mode;   /* 0 = auto, 1 = node-sharded (RCCL each round), 2 = partition-  */
-                          /*     component-sharded (no collective)                          */
+    int32_t shard_mode;   /* FIT_SHARD_*: how world > 1 ranks split one placement           */
     int32_t window_min;   /* jobs per component per round, lower bound (0 = default 256)   */
     int32_t window_max;   /* upper bound (0 = default 8192)                                 */
     int32_t flags;        /* reserved, 0                                                    */
+    fit_exchange_fn exchange;  /* NULL = RCCL over xGMI (nccl_id required)                  */
+    void* exchange_user;
 } fit_opts;
+
+#define FIT_SHARD_AUTO 0       /* components if there are at least `world` of them, else nodes */
+#define FIT_SHARD_NODES 1      /* every rank scans 1/world of every component's nodes; per     */
+                               /* round: allgather candidates + 64-bit min-allreduce of bounds */
+#define FIT_SHARD_COMPONENTS 2 /* ranks own whole partition components; one merge at the end   */
 
 typedef struct {
     int64_t jobs;          /* jobs in the call                                              */
@@ -75,6 +90,8 @@ typedef struct {
     double ms_scan;        /* device time in fit_scan (HIP events, summed over rounds)       */
     double ms_commit;      /* device time in fit_commit                                      */
     double ms_exchange;    /* device time in the RCCL exchange (world > 1)                   */
+    int32_t shard_mode;    /* mode used (FIT_SHARD_NODES / FIT_SHARD_COMPONENTS; 0 if world 1) */
+    int32_t components;    /* independent partition components                               */
 } fit_stats;
 
 /* ---- engine -------------------------------------------------------------------------- */

@@ -36,7 +36,7 @@ def _p(a, t):
 
 class ModelParams(C.Structure):
     _fields_ = [("slice", C.c_int32), ("ks", C.c_int32), ("km", C.c_int32), ("ucap", C.c_int32),
-                ("wmin", C.c_int32), ("wmax", C.c_int32)]
+                ("wmin", C.c_int32), ("wmax", C.c_int32), ("shards", C.c_int32)]
 
 
 def _prep(nodes, jobs, parts):
@@ -71,13 +71,13 @@ def ref_place(nodes, jobs, parts, kmax: int = 1):
     return out, stats, (cf, mf, gf)
 
 
-def model_place(nodes, jobs, parts, slice=2048, ks=8, km=32, ucap=256, wmin=256, wmax=65536):
+def model_place(nodes, jobs, parts, slice=2048, ks=8, km=32, ucap=256, wmin=256, wmax=65536, shards=1):
     """CPU model of the GPU round algorithm (k = 1 jobs)."""
     cf, mf, gf, av, mk, pt, jb, jp, _ = _prep(nodes, jobs, parts)
     j = jobs.j
     out = np.empty(j, np.int32)
     st = np.zeros(8, np.int64)
-    prm = ModelParams(slice, ks, km, ucap, wmin, wmax)
+    prm = ModelParams(slice, ks, km, ucap, wmin, wmax, shards)
     I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
     rc = lib().model_place(
         I32(nodes.n), _p(cf, I32), _p(mf, I32), _p(gf, I32), _p(av, I32), _p(mk, U32),

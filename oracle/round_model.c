@@ -19,6 +19,7 @@ typedef struct {
     int32_t km;        /* candidates kept per job after merge (<= 64) */
     int32_t ucap;      /* dirty-set capacity per component per round */
     int32_t wmin, wmax;/* window bounds (jobs per component per round) */
+    int32_t shards;    /* node shards per component (multi-GPU node sharding), >= 1 */
 } model_params;
 
 /* stats: [0] rounds [1] scan evals [2] dirty evals [3] stops_rescan [4] stops_ucap
@@ -136,7 +137,9 @@ int model_place(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_fr
     uint64_t* bound = malloc(sizeof(uint64_t) * (size_t)wcap);
     int32_t smax = 1;
     for (int c = 0; c < ncomp; c++) {
-        int32_t s = (nb[c + 1] - nb[c] + prm->slice - 1) / prm->slice;
+        const int32_t nsh = prm->shards > 1 ? prm->shards : 1;
+        const int32_t per = (nb[c + 1] - nb[c] + nsh - 1) / nsh;
+        int32_t s = nsh * ((per + prm->slice - 1) / prm->slice);
         if (s > smax) smax = s;
     }
     uint64_t* sl = malloc(sizeof(uint64_t) * (size_t)prm->ks);
@@ -163,8 +166,12 @@ int model_place(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_fr
                 int32_t q = jl[cursor[c] + t];
                 uint64_t B = KEY_INF;
                 int nm = 0;
-                for (int32_t s0 = n0; s0 < n1; s0 += prm->slice) {
-                    int32_t s1 = s0 + prm->slice < n1 ? s0 + prm->slice : n1;
+                const int32_t nsh = prm->shards > 1 ? prm->shards : 1;
+                const int32_t per = (n1 - n0 + nsh - 1) / nsh;
+                for (int32_t sh = 0; sh < nsh; ++sh)
+                for (int32_t s0 = n0 + sh * per; s0 < n0 + (sh + 1) * per && s0 < n1; s0 += prm->slice) {
+                    int32_t se = n0 + (sh + 1) * per < n1 ? n0 + (sh + 1) * per : n1;
+                    int32_t s1 = s0 + prm->slice < se ? s0 + prm->slice : se;
                     for (int i = 0; i < prm->ks; i++) sl[i] = KEY_INF;
                     int64_t feas = 0;
                     for (int32_t x = s0; x < s1; x++) {

@@ -135,7 +135,13 @@ double now_ms() {
 struct fit_ctx {
     int device = 0;
     int rank = 0, world = 1;
+    int shard_mode = FIT_SHARD_AUTO;
     ncclComm_t comm = nullptr;
+    fit_exchange_fn xchg = nullptr;  // host exchange instead of RCCL (tests, custom transport)
+    void* xchg_user = nullptr;
+    HBuf<uint8_t> h_x;               // staging for the host exchange
+    DBuf<uint64_t> xcount;           // per-rank counters (component-sharded stats)
+    HBuf<uint64_t> h_count;
     hipStream_t st = nullptr;
     hipEvent_t ev[6] = {};
     int wmin = 256, wmax = 8192;
@@ -188,6 +194,9 @@ struct fit_ctx {
         h_plan.release();
         h_res.release();
         h_jcomp.release();
+        h_x.release();
+        xcount.release();
+        h_count.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
@@ -266,6 +275,41 @@ int alloc_cols(fit_ctx* c, int32_t n) {
     return 0;
 }
 
+// ------------------------------------------------------------------------ exchange
+// In-place collectives on device buffers: RCCL over xGMI, or the caller's host exchange.
+int xchg(fit_ctx* c, int op, void* dbuf, int64_t count) {
+    if (c->world == 1 || count == 0) return 0;
+    if (!c->xchg) {
+        switch (op) {
+            case FIT_XCHG_ALLGATHER_U64: {
+                uint64_t* b = static_cast<uint64_t*>(dbuf);
+                NCCL_TRY(ncclAllGather(b + (size_t)c->rank * count, b, count, ncclUint64, c->comm,
+                                       c->st));
+                return 0;
+            }
+            case FIT_XCHG_MIN_U64:
+                NCCL_TRY(ncclAllReduce(dbuf, dbuf, count, ncclUint64, ncclMin, c->comm, c->st));
+                return 0;
+            case FIT_XCHG_MAX_I32:
+                NCCL_TRY(ncclAllReduce(dbuf, dbuf, count, ncclInt32, ncclMax, c->comm, c->st));
+                return 0;
+            case FIT_XCHG_MIN_I32:
+                NCCL_TRY(ncclAllReduce(dbuf, dbuf, count, ncclInt32, ncclMin, c->comm, c->st));
+                return 0;
+        }
+        return fail(FIT_E_INVAL, "exchange op %d", op);
+    }
+    const size_t elem = (op == FIT_XCHG_ALLGATHER_U64 || op == FIT_XCHG_MIN_U64) ? 8 : 4;
+    const size_t bytes = elem * (size_t)count * (op == FIT_XCHG_ALLGATHER_U64 ? c->world : 1);
+    if (c->h_x.ensure(bytes)) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->h_x.p, dbuf, bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (c->xchg(c->xchg_user, op, c->h_x.p, count) != 0)
+        return fail(FIT_E_RCCL, "host exchange op %d failed", op);
+    HIP_TRY(hipMemcpyAsync(dbuf, c->h_x.p, bytes, hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
 // ------------------------------------------------------------------------ placement
 int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
@@ -304,6 +348,33 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
                            st));
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
 
+    // world > 1: split by components (each rank owns whole components, no per-round exchange)
+    // or by nodes (north_star: every rank scans 1/world of every component, RCCL each round)
+    int mode = 0;
+    std::vector<char> owned(C, 1);
+    if (c->world > 1) {
+        mode = c->shard_mode;
+        if (mode == FIT_SHARD_AUTO) mode = C >= c->world ? FIT_SHARD_COMPONENTS : FIT_SHARD_NODES;
+        if (mode == FIT_SHARD_COMPONENTS) {
+            // LPT by work (jobs × nodes); identical on every rank (same inputs, same order)
+            std::vector<int> order(C);
+            for (int k = 0; k < C; ++k) order[k] = k;
+            auto work = [&](int k) { return (int64_t)(jb[k + 1] - jb[k]) * (c->nb[k + 1] - c->nb[k]); };
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return work(a) > work(b); });
+            std::vector<int64_t> load(c->world, 0);
+            for (int k : order) {
+                int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                load[r] += work(k) + 1;
+                owned[k] = r == c->rank;
+            }
+        }
+    }
+    S.shard_mode = mode;
+    S.components = C;
+    const bool node_sharded = mode == FIT_SHARD_NODES;
+    const int shards = node_sharded ? c->world : 1;
+    const int srank = node_sharded ? c->rank : 0;
+
     // 3. speculative rounds
     std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
     if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||
@@ -321,15 +392,15 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             P.nb = c->nb[k];
             P.ne = c->nb[k + 1];
             const int32_t len = P.ne - P.nb;
-            const int32_t per = (len + c->world - 1) / c->world;
-            P.sb = std::min(P.ne, P.nb + per * c->rank);
+            const int32_t per = (len + shards - 1) / shards;
+            P.sb = std::min(P.ne, P.nb + per * srank);
             P.se = std::min(P.ne, P.sb + per);
             // sub-slices of >= MIN_SUB nodes, at most MAX_SLICES block-slices per job per rank
             P.sub = std::max(MIN_SUB, (per + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
             P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
-            epl = std::max(epl, (c->world * P.nslice * KS + 63) / 64);
+            epl = std::max(epl, (shards * P.nslice * KS + 63) / 64);
             P.jbase = cur[k];
-            P.w = std::min(win[k], jb[k + 1] - cur[k]);
+            P.w = owned[k] ? std::min(win[k], jb[k + 1] - cur[k]) : 0;
             P.blk0 = (int32_t)blocks;
             P.cand_off = cand_n;
             P.slot0 = (int32_t)slots;
@@ -345,7 +416,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
         if (!any) break;
         S.rounds++;
         S.evals += evals;
-        if (c->cand.ensure((size_t)cand_n * c->world) || c->bnd.ensure(slots) ||
+        if (c->cand.ensure((size_t)cand_n * shards) || c->bnd.ensure(slots) ||
             c->wjob.ensure(slots))
             return FIT_E_OOM;
         HIP_TRY(hipMemcpyAsync(c->plan.p, c->h_plan.p, sizeof(CompPlan) * C, hipMemcpyHostToDevice,
@@ -353,17 +424,17 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
         HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * slots, st));
         HIP_TRY(hipEventRecord(c->ev[0], st));
         HIP_TRY(launch_scan((int)blocks, st, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
-                            c->plan.p, C, c->cand.p + (size_t)c->rank * cand_n, c->bnd.p,
+                            c->plan.p, C, c->cand.p + (size_t)srank * cand_n, c->bnd.p,
                             c->wjob.p));
         HIP_TRY(hipEventRecord(c->ev[1], st));
-        if (c->world > 1) {
+        if (node_sharded) {
             // every rank scanned its node shard: gather all candidate sections, min the bounds
-            NCCL_TRY(ncclAllGather(c->cand.p + (size_t)c->rank * cand_n, c->cand.p, cand_n,
-                                   ncclUint64, c->comm, st));
-            NCCL_TRY(ncclAllReduce(c->bnd.p, c->bnd.p, slots, ncclUint64, ncclMin, c->comm, st));
+            int rc = xchg(c, FIT_XCHG_ALLGATHER_U64, c->cand.p, cand_n);
+            if (!rc) rc = xchg(c, FIT_XCHG_MIN_U64, c->bnd.p, slots);
+            if (rc) return rc;
         }
         HIP_TRY(hipEventRecord(c->ev[2], st));
-        HIP_TRY(launch_commit(C, epl, lds, st, c->rec.p, c->plan.p, c->cand.p, cand_n, c->world,
+        HIP_TRY(launch_commit(C, epl, lds, st, c->rec.p, c->plan.p, c->cand.p, cand_n, shards,
                               c->bnd.p, c->wjob.p, out, kmax, c->res.p));
         HIP_TRY(hipEventRecord(c->ev[3], st));
         HIP_TRY(hipMemcpyAsync(c->h_res.p, c->res.p, sizeof(CommitResult) * C,
@@ -388,6 +459,24 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             int32_t nw = R.stop ? 2 * R.done : 2 * P.w;
             win[k] = std::max(c->wmin, std::min(c->wmax, nw));
         }
+    }
+    if (mode == FIT_SHARD_COMPONENTS) {
+        // each rank placed only its components: combine placements (owner's >= -1 beats -1;
+        // rejections are identical everywhere) and node rows (only owners lowered them)
+        int rc = xchg(c, FIT_XCHG_MAX_I32, out, (int64_t)J * kmax);
+        if (!rc) rc = xchg(c, FIT_XCHG_MIN_I32, c->rec.p, (int64_t)c->nn * 8);
+        if (rc) return rc;
+        // global placed count: allgather one u64 per rank, sum on the host
+        if (c->xcount.ensure(c->world) || c->h_count.ensure(c->world)) return FIT_E_OOM;
+        c->h_count.p[c->rank] = (uint64_t)S.placed;
+        HIP_TRY(hipMemcpyAsync(c->xcount.p + c->rank, c->h_count.p + c->rank, 8,
+                               hipMemcpyHostToDevice, st));
+        rc = xchg(c, FIT_XCHG_ALLGATHER_U64, c->xcount.p, 1);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(c->h_count.p, c->xcount.p, 8 * c->world, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        S.placed = 0;
+        for (int r = 0; r < c->world; ++r) S.placed += (int64_t)c->h_count.p[r];
     }
     // jobs of partitions without nodes are FIT_UNPLACED like jobs nothing fits
     S.unplaced = J - S.placed - S.rejected;
@@ -456,6 +545,9 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     c->device = dev;
     c->rank = o.rank;
     c->world = o.world;
+    c->shard_mode = o.shard_mode;
+    c->xchg = o.exchange;
+    c->xchg_user = o.exchange_user;
     if (o.window_min > 0) c->wmin = o.window_min;
     if (o.window_max > 0) c->wmax = std::max(o.window_max, c->wmin);
     for (int p = 0; p < 32; ++p) {
@@ -467,7 +559,7 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) rc = FIT_E_HIP;
     for (auto& e : c->ev)
         if (!rc && hipEventCreate(&e) != hipSuccess) rc = FIT_E_HIP;
-    if (!rc && c->world > 1) {
+    if (!rc && c->world > 1 && !c->xchg) {
         if (!o.nccl_id) {
             rc = fail(FIT_E_INVAL, "world > 1 needs nccl_id");
         } else {

@@ -24,14 +24,17 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (FIT_E_PARSE, FIT_E_UNLIMITED, FIT_REJECTED, FIT_UNPLACED, FitError, FitJobResources,
-                   FitNode, FitOpts, FitResources, FitStats, check, lib)
+from ._lib import (FIT_E_PARSE, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS,
+                   FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32,
+                   FIT_XCHG_MIN_U64, XCHG_FN, FitError, FitJobResources, FitNode, FitOpts, FitResources,
+                   FitStats, check, lib)
 
 __all__ = [
     "Engine", "FitError", "ErrDurationIsUnlimited", "ParseDuration", "parse_resources", "parse_nodes",
     "parse_partition", "parse_partitions_names", "extract_batch_resources", "apply_spec",
     "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
-    "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources",
+    "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
+    "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS",
 ]
 
 
@@ -182,14 +185,53 @@ def nccl_unique_id() -> bytes:
     return buf.raw
 
 
+class TorchHostExchange:
+    """Host-side exchange over torch.distributed (e.g. gloo) for the engine's collectives.
+
+    Lets several ranks share one GPU in tests, exercising exactly the multi-rank engine code that
+    RCCL drives in production (fit_opts.exchange, include/fitgpu.h)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.fn = XCHG_FN(self._call)
+
+    def _call(self, user, op, buf, count):
+        import torch
+        try:
+            d = self.dist
+            if op in (FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MIN_U64):
+                n = count * (self.world if op == FIT_XCHG_ALLGATHER_U64 else 1)
+                arr = np.ctypeslib.as_array(C.cast(buf, C.POINTER(C.c_int64)), shape=(n,))
+                mine = arr[self.rank * count:(self.rank + 1) * count] if op == FIT_XCHG_ALLGATHER_U64 else arr
+                parts = [torch.empty(count, dtype=torch.int64) for _ in range(self.world)]
+                d.all_gather(parts, torch.from_numpy(mine.copy()), group=self.group)
+                if op == FIT_XCHG_ALLGATHER_U64:
+                    arr[:] = torch.cat(parts).numpy()
+                else:
+                    arr[:] = np.minimum.reduce([p.numpy().view(np.uint64) for p in parts]).view(np.int64)
+            else:
+                arr = np.ctypeslib.as_array(C.cast(buf, C.POINTER(C.c_int32)), shape=(count,))
+                t = torch.from_numpy(arr.copy())
+                d.all_reduce(t, op=d.ReduceOp.MAX if op == FIT_XCHG_MAX_I32 else d.ReduceOp.MIN, group=self.group)
+                arr[:] = t.numpy()
+            return 0
+        except Exception:  # never let a Python exception cross the C boundary
+            return -1
+
+
 class Engine:
-    """One placement context on one GPU (optionally one rank of a node-sharded group)."""
+    """One placement context on one GPU (optionally one rank of a multi-GPU group)."""
 
     def __init__(self, device: int = -1, rank: int = 0, world: int = 1, nccl_id: bytes | None = None,
-                 window_min: int = 0, window_max: int = 0, shard_mode: int = 0):
+                 window_min: int = 0, window_max: int = 0, shard_mode: int = 0,
+                 exchange: "TorchHostExchange | None" = None):
         self._idbuf = C.create_string_buffer(nccl_id, 128) if nccl_id else None
+        self._xchg = exchange
         o = FitOpts(device, rank, world, C.cast(self._idbuf, C.c_void_p) if self._idbuf else None,
-                    shard_mode, window_min, window_max, 0)
+                    shard_mode, window_min, window_max, 0, exchange.fn if exchange else XCHG_FN(), None)
         h = C.c_void_p()
         check(lib().fit_create(C.byref(o), C.byref(h)), "fit_create")
         self._h = h

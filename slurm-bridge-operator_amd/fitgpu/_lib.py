@@ -34,10 +34,16 @@ EXPORTS = [
 ]
 
 
+XCHG_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64)
+FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MIN_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32 = 1, 2, 3, 4
+FIT_SHARD_AUTO, FIT_SHARD_NODES, FIT_SHARD_COMPONENTS = 0, 1, 2
+
+
 class FitOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32),
                 ("nccl_id", C.c_void_p), ("shard_mode", C.c_int32), ("window_min", C.c_int32),
-                ("window_max", C.c_int32), ("flags", C.c_int32)]
+                ("window_max", C.c_int32), ("flags", C.c_int32), ("exchange", XCHG_FN),
+                ("exchange_user", C.c_void_p)]
 
 
 class FitStats(C.Structure):
@@ -45,7 +51,8 @@ class FitStats(C.Structure):
                 ("rejected", C.c_int64), ("rounds", C.c_int64), ("evals", C.c_int64),
                 ("useful_evals", C.c_int64), ("stops_rescan", C.c_int64),
                 ("stops_dirty", C.c_int64), ("ms_total", C.c_double), ("ms_scan", C.c_double),
-                ("ms_commit", C.c_double), ("ms_exchange", C.c_double)]
+                ("ms_commit", C.c_double), ("ms_exchange", C.c_double), ("shard_mode", C.c_int32),
+                ("components", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

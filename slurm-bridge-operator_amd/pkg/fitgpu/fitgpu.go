@@ -1,0 +1,122 @@
+// Package fitgpu is the cgo binding a slurm-bridge-operator maintainer adds to call the MI355X
+// placement engine (libfitgpu.so, C-ABI include/fitgpu.h).  It is not compiled in this repo's
+// image (no Go toolchain); INTEGRATION.md shows where it is called from.
+package fitgpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../fitgpu -lfitgpu -Wl,-rpath,${SRCDIR}/../../fitgpu
+#include <stdlib.h>
+#include "fitgpu.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"runtime"
+	"unsafe"
+)
+
+const (
+	Unplaced = -1 // FIT_UNPLACED
+	Rejected = -2 // FIT_REJECTED
+)
+
+// Error carries a negative FIT_E_* code and the library's detail message.
+type Error struct {
+	Code   int
+	Detail string
+}
+
+func (e *Error) Error() string {
+	return fmt.Sprintf("fitgpu: %s (%d): %s", C.GoString(C.fit_strerror(C.int(e.Code))), e.Code, e.Detail)
+}
+
+func check(rc C.int) error {
+	if rc < 0 {
+		return &Error{Code: int(rc), Detail: C.GoString(C.fit_last_error())}
+	}
+	return nil
+}
+
+// Engine wraps one fit_ctx (one GPU).  Not safe for concurrent use; the VK provider serialises
+// its 10 PodSyncWorkers through a batcher (INTEGRATION.md).
+type Engine struct{ ctx *C.fit_ctx }
+
+func New(device int) (*Engine, error) {
+	opts := C.fit_opts{device: C.int32_t(device), world: 1}
+	var ctx *C.fit_ctx
+	if err := check(C.fit_create(&opts, &ctx)); err != nil {
+		return nil, err
+	}
+	e := &Engine{ctx: ctx}
+	runtime.SetFinalizer(e, func(e *Engine) { e.Close() })
+	return e, nil
+}
+
+func (e *Engine) Close() {
+	if e.ctx != nil {
+		C.fit_destroy(e.ctx)
+		e.ctx = nil
+	}
+}
+
+// Nodes is the node table in Client.Nodes order (pkg/slurm-agent/slurm.go:343-364).
+type Nodes struct {
+	CPUFree, MemFreeMiB, GPUFree, AvailMin []int32
+	PartMask                              []uint32
+}
+
+func (e *Engine) LoadNodes(n Nodes) error {
+	cnt := len(n.CPUFree)
+	if cnt == 0 {
+		return check(C.fit_load_nodes(e.ctx, 0, nil, nil, nil, nil, nil))
+	}
+	// slices of plain integers: no Go pointers inside, the library copies and does not retain
+	return check(C.fit_load_nodes(e.ctx, C.int32_t(cnt),
+		(*C.int32_t)(unsafe.Pointer(&n.CPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.MemFreeMiB[0])),
+		(*C.int32_t)(unsafe.Pointer(&n.GPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.AvailMin[0])),
+		(*C.uint32_t)(unsafe.Pointer(&n.PartMask[0]))))
+}
+
+// LoadPartitions takes parseResources' limits (pkg/slurm-agent/parse.go:111-190), -1 = UNLIMITED.
+func (e *Engine) LoadPartitions(maxTimeMin, maxCPUs, maxMemMiB []int32) error {
+	p := len(maxTimeMin)
+	if p == 0 {
+		return check(C.fit_load_partitions(e.ctx, 0, nil, nil, nil))
+	}
+	return check(C.fit_load_partitions(e.ctx, C.int32_t(p), (*C.int32_t)(unsafe.Pointer(&maxTimeMin[0])),
+		(*C.int32_t)(unsafe.Pointer(&maxCPUs[0])), (*C.int32_t)(unsafe.Pointer(&maxMemMiB[0]))))
+}
+
+// Jobs in priority order, per-node demand (DESIGN.md §2).
+type Jobs struct {
+	CPU, MemMiB, GPU, WallMin []int32
+	Part, NodesK              []uint16
+}
+
+type Stats = C.fit_stats
+
+// Place returns node ids (or Unplaced / Rejected) per job, kmax entries per job.
+func (e *Engine) Place(j Jobs, kmax int) ([]int32, Stats, error) {
+	cnt := len(j.CPU)
+	out := make([]int32, cnt*kmax)
+	var st C.fit_stats
+	if cnt == 0 {
+		return out, st, nil
+	}
+	rc := C.fit_place(e.ctx, C.int32_t(cnt), (*C.int32_t)(unsafe.Pointer(&j.CPU[0])),
+		(*C.int32_t)(unsafe.Pointer(&j.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&j.GPU[0])),
+		(*C.int32_t)(unsafe.Pointer(&j.WallMin[0])), (*C.uint16_t)(unsafe.Pointer(&j.Part[0])),
+		(*C.uint16_t)(unsafe.Pointer(&j.NodesK[0])), C.int32_t(kmax),
+		(*C.int32_t)(unsafe.Pointer(&out[0])), &st)
+	return out, st, check(rc)
+}
+
+// PartitionFree is the allocation-aware replacement for GetPartitionCapacity's sum
+// (pkg/slurm-virtual-kubelet/node.go:183-190).
+func (e *Engine) PartitionFree(p int) (cpu, memMiB, gpu int64, err error) {
+	var c, m, g C.int64_t
+	err = check(C.fit_partition_free(e.ctx, C.int32_t(p), &c, &m, &g))
+	return int64(c), int64(m), int64(g), err
+}
