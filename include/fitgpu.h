@@ -87,9 +87,12 @@ typedef struct {
     int64_t stops_rescan;  /* round cut because a job's candidate list ran out               */
     int64_t stops_dirty;   /* round cut because the dirty-node set was full                  */
     double ms_total;       /* wall time of the call on the host clock                        */
-    double ms_scan;        /* device time in fit_scan (HIP events, summed over rounds)       */
-    double ms_commit;      /* device time in fit_commit                                      */
+    double ms_scan;        /* scan time: k_scan launches (host loop) or the average scan-   */
+                           /* worker busy time inside the persistent engine                 */
+    double ms_commit;      /* commit time: k_commit launches, or the slowest component's     */
+                           /* committer inside the persistent engine                        */
     double ms_exchange;    /* device time in the RCCL exchange (world > 1)                   */
+    double ms_device;      /* device time of the placement launches (HIP events)             */
     int32_t shard_mode;    /* mode used (FIT_SHARD_NODES / FIT_SHARD_COMPONENTS; 0 if world 1) */
     int32_t components;    /* independent partition components                               */
 } fit_stats;

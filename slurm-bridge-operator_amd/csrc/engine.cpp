@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -38,6 +39,16 @@ hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t
                                const int32_t* perm, int32_t nn, NodeRec* rec);
 hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, int32_t* cpu,
                                 int32_t* mem, int32_t* gpu);
+size_t engine_lds_bytes(int32_t max_component_nodes);
+size_t engine_ctl_bytes();
+size_t engine_ring_bytes();
+int engine_blocks_per_cu(size_t lds);
+hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
+                         const void* cs, void* co, CompPlan* plans, int ncomp, NodeRec* rec,
+                         const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
+                         const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                         const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
+                         int32_t* out, int kmax, int64_t* wbusy);
 }  // namespace fitgpu
 
 using namespace fitgpu;
@@ -141,6 +152,16 @@ struct fit_ctx {
     void* xchg_user = nullptr;
     HBuf<uint8_t> h_x;               // staging for the host exchange
     DBuf<uint64_t> xcount;           // per-rank counters (component-sharded stats)
+    bool persistent = true;          // one-launch work-queue engine (FIT_ENGINE=rounds: host loop)
+    int cus = 256;
+    DBuf<uint8_t> ectl, ering;
+    DBuf<CompState> ecs;
+    DBuf<CompOut> eco;
+    DBuf<int64_t> ebusy;
+    HBuf<CompState> h_ecs;
+    HBuf<CompOut> h_eco;
+    HBuf<int64_t> h_ebusy;
+    HBuf<uint32_t> h_err;
     HBuf<uint64_t> h_count;
     hipStream_t st = nullptr;
     hipEvent_t ev[6] = {};
@@ -197,6 +218,15 @@ struct fit_ctx {
         h_x.release();
         xcount.release();
         h_count.release();
+        ectl.release();
+        ering.release();
+        ecs.release();
+        eco.release();
+        ebusy.release();
+        h_ecs.release();
+        h_eco.release();
+        h_ebusy.release();
+        h_err.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
@@ -310,6 +340,93 @@ int xchg(fit_ctx* c, int op, void* dbuf, int64_t count) {
     return 0;
 }
 
+// ------------------------------------------------------------- persistent engine path
+// All rounds of all owned components in one launch (fit_persistent.hip).
+int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector<char>& owned,
+                   const int32_t* cpu, const int32_t* mem, const int32_t* gpu, const int32_t* wall,
+                   const uint16_t* part, const uint16_t* nk, int32_t* out, int32_t kmax,
+                   fit_stats& S) {
+    const int C = c->ncomp;
+    hipStream_t st = c->st;
+    std::vector<int> comps;
+    int32_t maxnodes = 0;
+    for (int k = 0; k < C; ++k)
+        if (owned[k] && jb[k + 1] > jb[k]) {
+            comps.push_back(k);
+            maxnodes = std::max(maxnodes, c->nb[k + 1] - c->nb[k]);
+        }
+    const int nc = (int)comps.size();
+    if (nc == 0) return 0;
+    const int64_t wcap = c->wmax;
+    const int64_t per_comp_cand = wcap * MAX_SLICES * KS;
+    if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
+        c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
+        c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
+        c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
+        c->h_err.ensure(4))
+        return FIT_E_OOM;
+    for (int i = 0; i < nc; ++i) {
+        const int k = comps[i];
+        CompState& s = c->h_ecs.p[i];
+        s.nb = s.sb = c->nb[k];
+        s.ne = s.se = c->nb[k + 1];
+        const int32_t len = s.ne - s.nb;
+        s.sub = std::max(MIN_SUB, (len + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
+        s.nslice = std::max(1, (len + SCAN_WAVES * s.sub - 1) / (SCAN_WAVES * s.sub));
+        s.jstart = jb[k];
+        s.jend = jb[k + 1];
+        s.cand_off = (int64_t)i * per_comp_cand;
+        s.slot0 = (int32_t)(i * wcap);
+        s.wmin = c->wmin;
+        s.wmax = c->wmax;
+    }
+    const size_t lds = engine_lds_bytes(maxnodes);
+    int per_cu = engine_blocks_per_cu(lds);
+    if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine does not fit on a CU (lds %zu)", lds);
+    // every block must be resident (workers and committers spin on each other): stay one block
+    // per CU below the occupancy answer (it can over-report by one; MI355X_MICROARCH.md)
+    const int resident = std::max(1, per_cu - 1) * c->cus;
+    const int workers = std::max(8, resident - nc);
+    if (c->ebusy.ensure(workers) || c->h_ebusy.ensure(workers)) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
+    HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    HIP_TRY(launch_engine(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
+                          c->plan.p, nc, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
+                          c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p));
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * workers,
+                           hipMemcpyDeviceToHost, st));
+    // error word: EngineCtl::error sits at byte offset 2 * 128 + 4
+    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_err.p[0]) return fail(FIT_E_HIP, "placement engine watchdog tripped (code %u)", c->h_err.p[0]);
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    S.ms_device += ms;
+    int64_t busy = 0;
+    for (int i = 0; i < workers; ++i) busy += c->h_ebusy.p[i];
+    S.ms_scan += busy / 1e5 / workers;  // average worker busy time (100 MHz ticks)
+    double commit_max = 0;
+    for (int i = 0; i < nc; ++i) {
+        const CompOut& o = c->h_eco.p[i];
+        const int k = comps[i];
+        if (o.done_jobs != jb[k + 1] - jb[k])
+            return fail(FIT_E_HIP, "component %d resolved %lld of %d jobs", k, (long long)o.done_jobs,
+                        jb[k + 1] - jb[k]);
+        S.evals += o.evals;
+        S.placed += o.placed;
+        S.rounds = std::max<int64_t>(S.rounds, o.rounds);
+        S.stops_rescan += o.stops_rescan;
+        S.stops_dirty += o.stops_dirty;
+        commit_max = std::max(commit_max, o.t_commit / 1e5);
+    }
+    S.ms_commit += commit_max;
+    return 0;
+}
+
 // ------------------------------------------------------------------------ placement
 int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
@@ -375,7 +492,12 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     const int shards = node_sharded ? c->world : 1;
     const int srank = node_sharded ? c->rank : 0;
 
-    // 3. speculative rounds
+    // 3. speculative rounds: one persistent launch, or the host-driven loop (node sharding
+    // exchanges candidates over RCCL every round, so it keeps the host loop)
+    if (c->persistent && !node_sharded) {
+        int rc = run_persistent(c, jb, owned, cpu, mem, gpu, wall, part, nk, out, kmax, S);
+        if (rc) return rc;
+    } else {
     std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
     if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||
         c->h_res.ensure(C + 1))
@@ -460,6 +582,8 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             win[k] = std::max(c->wmin, std::min(c->wmax, nw));
         }
     }
+    S.ms_device = S.ms_scan + S.ms_exchange + S.ms_commit;
+    }  // host-driven rounds
     if (mode == FIT_SHARD_COMPONENTS) {
         // each rank placed only its components: combine placements (owner's >= -1 beats -1;
         // rejections are identical everywhere) and node rows (only owners lowered them)
@@ -543,6 +667,8 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     fit_ctx* c = new (std::nothrow) fit_ctx();
     if (!c) return fail(FIT_E_OOM, "context allocation");
     c->device = dev;
+    c->cus = prop.multiProcessorCount;
+    if (const char* ev = getenv("FIT_ENGINE")) c->persistent = strcmp(ev, "rounds") != 0;
     c->rank = o.rank;
     c->world = o.world;
     c->shard_mode = o.shard_mode;

@@ -43,6 +43,21 @@ struct alignas(16) CompPlan {
     int32_t slot0;       // first window slot (global over components)
 };
 
+// Persistent engine (fit_persistent.hip): per-component state written by the host, results
+// written by the component's committer wave.
+struct CompState {
+    int32_t nb, ne, sb, se, nslice, sub;
+    int32_t jstart, jend;  // component job list range
+    int64_t cand_off;      // fixed candidate region of this component
+    int32_t slot0;         // fixed window slot region
+    int32_t wmin, wmax;
+};
+
+struct CompOut {
+    int64_t evals, placed, done_jobs, rounds, stops_rescan, stops_dirty;
+    int64_t t_commit, t_wait;  // 100 MHz realtime ticks spent committing / waiting for scans
+};
+
 struct CommitResult {
     int32_t done;   // jobs resolved this round (prefix of the window)
     int32_t stop;   // 0 window exhausted, 1 candidate list ran out, 2 dirty set full

@@ -9,120 +9,10 @@
 //              job exactly against (clean candidates ∪ dirty nodes): the speculative-prefix
 //              commit.  Dirty rows live in VGPRs (≤ 4 per lane), membership in an LDS bitmap.
 // The sequential semantics they reproduce bit-exactly is oracle/fitref.c:ref_place.
-#include <hip/hip_runtime.h>
-
-#include <type_traits>
-
-#include "fit_device.h"
+#include "fit_common.h"
 
 namespace fitgpu {
 
-__device__ __forceinline__ uint64_t fit_key(int32_t cf, int32_t mf, int32_t gf, int32_t av,
-                                            uint32_t mask, uint32_t pos, const JobRec& J) {
-    const int32_t dc = cf - J.cpu, dm = mf - J.mem, dg = gf - J.gpu, da = av - J.wall;
-    const bool ok = (dc | dm | dg | da) >= 0 && (mask & J.pbit);
-    const uint32_t sc = (min((uint32_t)dg, 255u) << 24) | (min((uint32_t)dc, 4095u) << 12) |
-                        min((uint32_t)dm >> 10, 4095u);
-    return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
-}
-
-// ---- wave-wide reductions (DPP; call with a full EXEC mask) ---------------------------
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
-    return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, CTRL, ROWMASK,
-                                                        0xf, false));
-}
-
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = dpp_min<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-    v = dpp_min<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-    v = dpp_min<0x124, 0xf>(v);  // row_ror:4
-    v = dpp_min<0x128, 0xf>(v);  // row_ror:8
-    v = dpp_min<0x142, 0xa>(v);  // row_bcast:15
-    v = dpp_min<0x143, 0xc>(v);  // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// min over the wave of a packed (score << 32 | position) key: 32-bit min of the scores, then of
-// the positions among the lanes holding that score (usually one lane: a readlane).
-__device__ __forceinline__ uint64_t wave_min_key(uint64_t v) {
-    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    const uint32_t mh = wave_min_u32(hi);
-    const uint64_t eq = __ballot(hi == mh);
-    uint32_t ml;
-    if (__popcll(eq) == 1)
-        ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(eq));
-    else
-        ml = wave_min_u32(hi == mh ? lo : 0xffffffffu);
-    return ((uint64_t)mh << 32) | ml;
-}
-
-__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
-__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
-
-// sorted ascending insert of x into key[0..KS) dropping the largest (static indices only)
-__device__ __forceinline__ void topk_insert(uint64_t (&key)[KS], uint64_t x) {
-#pragma unroll
-    for (int i = KS - 1; i > 0; --i) key[i] = umax64(key[i - 1], umin64(key[i], x));
-    key[0] = umin64(key[0], x);
-}
-
-// (list, bound) pairs: every node of the covered range that is not in the sorted list has a
-// key > bound, and every list entry is <= bound (bound = last entry, INF when not full).
-// Merge two such pairs over disjoint ranges into the pair for the union (bitonic, registers).
-__device__ __forceinline__ void merge_lists(uint64_t (&a)[KS], const uint64_t (&b)[KS]) {
-    const uint64_t bb = umin64(a[KS - 1], b[KS - 1]);
-    uint64_t c[KS];
-#pragma unroll
-    for (int i = 0; i < KS; ++i) {
-        const uint64_t x = a[i] > bb ? KEY_INF : a[i];
-        const uint64_t y = b[KS - 1 - i] > bb ? KEY_INF : b[KS - 1 - i];
-        c[i] = umin64(x, y);  // bitonic sequence holding the KS smallest of the union
-    }
-#pragma unroll
-    for (int st = KS / 2; st >= 1; st >>= 1)
-#pragma unroll
-        for (int i = 0; i < KS; ++i)
-            if ((i & st) == 0) {
-                const uint64_t lo = umin64(c[i], c[i + st]), hi = umax64(c[i], c[i + st]);
-                c[i] = lo;
-                c[i + st] = hi;
-            }
-#pragma unroll
-    for (int i = 0; i < KS; ++i) a[i] = c[i];
-    // The bound stays "last entry": if bb is finite, the list achieving it is full with all its
-    // KS entries <= bb, so the merged list is full and c[KS-1] <= bb is the new bound.
-}
-
-__device__ __forceinline__ int find_comp(const CompPlan* __restrict__ plan, int ncomp, int b) {
-    int c = 0;
-    for (int i = 1; i < ncomp; ++i)
-        if (plan[i].blk0 <= b) c = i;
-    return c;
-}
-
-// One (job-lane, node-row) evaluation.  Node fields are clamped to >= -1 when the table is built
-// (k_gather_nodes) and demands are >= 0, so every difference below is exact in int32; the pair
-// is feasible iff no difference is negative and the partition bit is set.
-__device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& J,
-                                         uint64_t (&key)[KS], uint32_t& lim) {
-    const int32_t dc = r.cpu - J.cpu, dm = r.mem - J.mem, dg = r.gpu - J.gpu;
-    const int32_t da = r.avail - J.wall;
-    const int32_t dp = (int32_t)((r.mask & J.pbit) - 1u);  // -1: not a member (or idle lane)
-    const int32_t bad = dc | dm | dg | da | dp;
-    const uint32_t sc = (min((uint32_t)dg, 255u) << 24) | (min((uint32_t)dc, 4095u) << 12) |
-                        min((uint32_t)dm >> 10, 4095u);
-    if (bad >= 0 && sc <= lim) {
-        topk_insert(key, ((uint64_t)sc << 32) | (uint32_t)x);
-        const uint64_t last = key[KS - 1];
-        lim = last == KEY_INF ? 0xffffffffu : (uint32_t)(last >> 32) - 1u;
-    }
-}
-
-// -------------------------------------------------------------------------------- k_scan
-// Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices (one per wave).
-// Each wave keeps the exact top-KS of its sub-slice; the 8 lists are merged through LDS in a
-// bitonic tree, giving the exact top-KS (and bound) of the block-slice.
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan(
     const NodeRec* __restrict__ rec, const int32_t* __restrict__ jl,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
@@ -137,230 +27,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan(
     // integer division expands to VALU code: pin the (uniform) results to SGPRs
     const int tile = __builtin_amdgcn_readfirstlane(local / P.nslice);
     const int s = __builtin_amdgcn_readfirstlane(local - tile * P.nslice);
-    if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    const int t = tile * SCAN_JOBS + lane;
-    const bool active = t < P.w;
-
-    JobRec J;
-    J.q = active ? jl[P.jbase + t] : 0;
-    J.cpu = active ? jcpu[J.q] : 0;
-    J.mem = active ? jmem[J.q] : 0;
-    J.gpu = active ? jgpu[J.q] : 0;
-    J.wall = active ? jwall[J.q] : 0;
-    J.pbit = active ? (1u << jpart[J.q]) : 0u;  // 0 → nothing feasible
-    J.k = active ? (jk ? max((int)jk[J.q], 1) : 1) : 1;
-    J.pad = 0;
-
-    uint64_t key[KS];
-#pragma unroll
-    for (int i = 0; i < KS; ++i) key[i] = KEY_INF;
-    // candidate test: score <= lim, lim = (K-th score - 1) once the list is full.  An equal
-    // score never beats the K-th entry (positions only grow); a spurious insert when the K-th
-    // score is 0 is dropped by the 64-bit insertion network, so the list stays exact.
-    uint32_t lim = 0xffffffffu;
-    const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
-    const int n1 = min(P.se, n0 + P.sub);
-    int x = n0;
-    for (; x + 4 <= n1; x += 4) {  // 4 rows per batch: four scalar row loads per wait
-        NodeRec r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = rec[x + u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
-    }
-    for (; x < n1; ++x) scan_row(rec[x], x, J, key, lim);
-
-    // merge tree: waves [h, 2h) hand their lists to waves [0, h)
-#pragma unroll
-    for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
-        if (wave >= h && wave < 2 * h) {
-#pragma unroll
-            for (int i = 0; i < KS; ++i) xk[wave - h][i][lane] = key[i];
-        }
-        __syncthreads();
-        if (wave < h) {
-            uint64_t o[KS];
-#pragma unroll
-            for (int i = 0; i < KS; ++i) o[i] = xk[wave][i][lane];
-            merge_lists(key, o);
-        }
-        __syncthreads();
-    }
-    if (wave != 0 || !active) return;
-    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KS;
-#pragma unroll
-    for (int i = 0; i < KS; i += 2) {
-        ulonglong2 v;
-        v.x = key[i];
-        v.y = key[i + 1];
-        *reinterpret_cast<ulonglong2*>(dst + i) = v;
-    }
-    if (key[KS - 1] != KEY_INF)
-        atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
-                  (unsigned long long)key[KS - 1]);
-    if (s == 0) wjob[P.slot0 + t] = J;
+    scan_tile<false>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk);
 }
-// ------------------------------------------------------------------------------ k_commit
-// One wave per component walks the window in priority order.  For job t it needs
-//   clean best  = min over its candidate entries <= B whose node is not dirty (LDS bitmap),
-//   dirty best  = min over the dirty rows (held in VGPRs, UPL per lane) at their current state,
-// then commits min(clean, dirty) or stops the round.  The candidate keys, job
-// row and bound are loaded two jobs ahead and the candidates' node rows one job ahead, so the
-// serial chain per job is LDS + VALU + one wave reduction.
-constexpr int UPL = UCAP / 64;  // dirty slots per lane
-
-// ---- diagnostic in-kernel stamps (only in the FIT_STAMPS build; never in the shipped kernel)
-#ifdef FIT_STAMPS
-__device__ unsigned long long g_stamps[64][8];
-#define STAMP_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long st_prev = 0; \
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
-#define STAMP(i)                                                                          \
-    do {                                                                                  \
-        __builtin_amdgcn_sched_barrier(0);                                                \
-        unsigned long long now_;                                                          \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");      \
-        __builtin_amdgcn_sched_barrier(0);                                                \
-        if (i > 0) st_acc[(i) > 0 ? (i) - 1 : 0] += now_ - st_prev;                                     \
-        st_prev = now_;                                                                   \
-    } while (0)
-#define STAMP_FLUSH(c, n)                                                                 \
-    {                                                                                     \
-        const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                      \
-        const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime();                  \
-        if (threadIdx.x == 0) {                                                           \
-            for (int i_ = 0; i_ < 6; ++i_) g_stamps[c][i_] = st_acc[i_];                  \
-            g_stamps[c][6] = n;                                                           \
-            g_stamps[c][7] = ((t1_ - st_t0) << 24) / max(r1_ - st_r0, 1ull); /* cyc/10ns << 24 */ \
-        }                                                                                 \
-    }
-#else
-#define STAMP_DECL
-#define STAMP(i)
-#define STAMP_FLUSH(c, n)
-#endif
-
-struct CRow {  // node row of a candidate (prefetched)
-    int32_t cpu, mem, gpu, avail;
-    uint32_t mask;
-    int32_t orig;
-};
-
-// Pipeline.  Iteration t: vector-load the keys of job t+2; derive the clean
-// flags of job t+1 (bound + dirty bitmap, before job t's commit); resolve job t; clear the flag
-// of any job-(t+1) candidate equal to the node job t dirtied; scalar-load job t+3's row and
-// bound.  Every wait is then on data requested at least one iteration earlier.  The 4-slot
-// job ring is indexed by literal constants only (4-way unrolled loop) so it stays in registers.
-#define FIT_COMMIT_STEP(A, N1, N2, N3)                                                            \
-    {                                                                                           \
-        if (t >= P.w) goto done;                                                                \
-        STAMP(0);                                                                               \
-        {                                                                                       \
-            const int tc_ = min(t + 2, wlast);                                                  \
-            _Pragma("unroll") for (int k = 0; k < EPL; ++k) kr[N2][k] =                         \
-                cand[off[k] + (int64_t)tc_ * per_rank];                                         \
-        }                                                                                       \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) {                                       \
-            const uint64_t kk_ = kr[N1][k];                                                     \
-            const bool v_ = has[k] && kk_ <= jb[N1] && kk_ != KEY_INF;                          \
-            const uint32_t rel_ = v_ ? (uint32_t)kk_ - nb : 0u;                                 \
-            cl[N1][k] = v_ && !((bitmap[rel_ >> 5] >> (rel_ & 31)) & 1u);                       \
-        }                                                                                       \
-        STAMP(1);                                                                               \
-        const int32_t jc = jcr[A], jm = jmr[A], jg = jgr[A], jw = jwr[A];                       \
-        const uint32_t jp = jpr[A];                                                             \
-        const uint64_t B = jb[A];                                                               \
-        uint64_t cm = KEY_INF;                                                                  \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) cm =                                    \
-            umin64(cm, cl[A][k] ? kr[A][k] : KEY_INF);                                          \
-        STAMP(2);                                                                               \
-        uint64_t dk[UPL];                                                                       \
-        uint64_t dm = KEY_INF;                                                                  \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) {                                       \
-            dk[i] = KEY_INF;                                                                    \
-            if (i * 64 < nu) {                                                                  \
-                const int32_t dc = ucpu[i] - jc, dmm = umem[i] - jm;                            \
-                const int32_t dg = ugpu[i] - jg, da = uav[i] - jw;                              \
-                const bool ok = (dc | dmm | dg | da) >= 0 && (umask[i] & jp) &&                 \
-                                i * 64 + lane < nu;                                             \
-                const uint32_t sc = (min((uint32_t)dg, 255u) << 24) |                           \
-                                    (min((uint32_t)dc, 4095u) << 12) |                          \
-                                    min((uint32_t)dmm >> 10, 4095u);                            \
-                dk[i] = ok ? (((uint64_t)sc << 32) | upos[i]) : KEY_INF;                        \
-                dm = umin64(dm, dk[i]);                                                         \
-            }                                                                                   \
-        }                                                                                       \
-        STAMP(3);                                                                               \
-        const uint64_t best = wave_min_key(umin64(cm, dm));                                     \
-        STAMP(4);                                                                               \
-        if (B != KEY_INF && best > B && __ballot(cm != KEY_INF) == 0ull) {                      \
-            stop = 1; /* candidate list exhausted: rescan next round */                         \
-            goto done;                                                                          \
-        }                                                                                       \
-        int32_t node = -1;                                                                      \
-        uint32_t newpos = 0xffffffffu;                                                          \
-        if (best != KEY_INF) {                                                                  \
-            const uint64_t dmask = __ballot(dm == best);                                        \
-            if (dmask) { /* a dirty row wins: update it in place */                             \
-                int32_t o = 0;                                                                  \
-                _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {              \
-                    const bool hit_ = dk[i] == best;                                            \
-                    ucpu[i] -= hit_ ? jc : 0;                                                   \
-                    umem[i] -= hit_ ? jm : 0;                                                   \
-                    ugpu[i] -= hit_ ? jg : 0;                                                   \
-                    o = hit_ ? uorig[i] : o;                                                    \
-                }                                                                               \
-                node = __builtin_amdgcn_readlane(o, __builtin_ctzll(dmask));                    \
-            } else { /* a clean candidate wins: its row becomes dirty row nu */                 \
-                if (nu == UCAP) {                                                               \
-                    stop = 2;                                                                   \
-                    goto done;                                                                  \
-                }                                                                               \
-                newpos = (uint32_t)best;                                                        \
-                const NodeRec r = rec[newpos];                                                  \
-                node = r.orig;                                                                  \
-                if (lane == (nu & 63)) {                                                        \
-                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i == (nu >> 6)) {       \
-                        ucpu[i] = r.cpu - jc;                                                   \
-                        umem[i] = r.mem - jm;                                                   \
-                        ugpu[i] = r.gpu - jg;                                                   \
-                        uav[i] = r.avail;                                                       \
-                        umask[i] = r.mask;                                                      \
-                        upos[i] = newpos;                                                       \
-                        uorig[i] = node;                                                        \
-                    }                                                                           \
-                    const uint32_t rel = newpos - nb;                                           \
-                    bitmap[rel >> 5] |= 1u << (rel & 31);                                       \
-                }                                                                               \
-                ++nu;                                                                           \
-            }                                                                                   \
-            ++placed;                                                                           \
-        }                                                                                       \
-        STAMP(5);                                                                               \
-        if (lane == (t & 63)) {                                                                 \
-            oq = jqr[A];                                                                        \
-            ov = node;                                                                          \
-        }                                                                                       \
-        if ((t & 63) == 63) { /* uniform: flush 64 placements */                                \
-            if (oq >= 0) out[(int64_t)oq * kmax] = ov;                                          \
-            oq = -1;                                                                            \
-        }                                                                                       \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) cl[N1][k] =                             \
-            cl[N1][k] && (uint32_t)kr[N1][k] != newpos;                                         \
-        {                                                                                       \
-            const int tc_ = min(t + 3, wlast); /* slot N3 (job t-1's) receives job t+3 */       \
-            const JobRec J_ = wjob[P.slot0 + tc_];                                              \
-            jqr[N3] = J_.q;                                                                     \
-            jcr[N3] = J_.cpu;                                                                   \
-            jmr[N3] = J_.mem;                                                                   \
-            jgr[N3] = J_.gpu;                                                                   \
-            jwr[N3] = J_.wall;                                                                  \
-            jpr[N3] = J_.pbit;                                                                  \
-            jb[N3] = bnd[P.slot0 + tc_];                                                        \
-        }                                                                                       \
-        ++t;                                                                                    \
-    }
 
 template <int EPL>
 __global__ __launch_bounds__(64) void k_commit(
@@ -371,88 +39,14 @@ __global__ __launch_bounds__(64) void k_commit(
     extern __shared__ uint32_t bitmap[];
     const int c = blockIdx.x;
     const CompPlan P = plan[c];
-    const int lane = threadIdx.x;
     if (P.w == 0) {
-        if (lane == 0) res[c] = CommitResult{0, 0, 0, 0};
+        if (threadIdx.x == 0) res[c] = CommitResult{0, 0, 0, 0};
         return;
     }
-    const int nwords = (P.ne - P.nb + 31) >> 5;
-    for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
-    __syncthreads();
-
-    const int per_rank = P.nslice * KS;
-    const int E = nranks * per_rank;
-    int64_t off[EPL];
-    bool has[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-        const int e = lane + 64 * k;
-        const int g = e / per_rank;
-        has[k] = e < E;
-        off[k] = has[k] ? g * rank_stride + P.cand_off + (e - g * per_rank) : P.cand_off;
-    }
-    const int wlast = P.w - 1;
-    const uint32_t nb = (uint32_t)P.nb;
-
-    int32_t ucpu[UPL], umem[UPL], ugpu[UPL], uav[UPL], uorig[UPL];
-    uint32_t umask[UPL], upos[UPL];
-#pragma unroll
-    for (int i = 0; i < UPL; ++i) {
-        ucpu[i] = umem[i] = ugpu[i] = uav[i] = uorig[i] = 0;
-        umask[i] = upos[i] = 0u;
-    }
-    int nu = 0, placed = 0, stop = 0, t = 0;
-    int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
-
-    uint64_t kr[4][EPL];
-    bool cl[4][EPL];
-    int32_t jqr[4], jcr[4], jmr[4], jgr[4], jwr[4];
-    uint32_t jpr[4];
-    uint64_t jb[4];
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int tc = min(s, wlast);
-        if (s < 2) {
-#pragma unroll
-            for (int k = 0; k < EPL; ++k) kr[s][k] = cand[off[k] + (int64_t)tc * per_rank];
-        }
-        const JobRec J = wjob[P.slot0 + tc];
-        jqr[s] = J.q;
-        jcr[s] = J.cpu;
-        jmr[s] = J.mem;
-        jgr[s] = J.gpu;
-        jwr[s] = J.wall;
-        jpr[s] = J.pbit;
-        jb[s] = bnd[P.slot0 + tc];
-    }
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-        const bool v = has[k] && kr[0][k] <= jb[0] && kr[0][k] != KEY_INF;
-        const uint32_t rel = v ? (uint32_t)kr[0][k] - nb : 0u;
-        cl[0][k] = v && !((bitmap[rel >> 5] >> (rel & 31)) & 1u);
-    }
-    STAMP_DECL
-    for (;;) {
-        FIT_COMMIT_STEP(0, 1, 2, 3)
-        FIT_COMMIT_STEP(1, 2, 3, 0)
-        FIT_COMMIT_STEP(2, 3, 0, 1)
-        FIT_COMMIT_STEP(3, 0, 1, 2)
-    }
-done:
-    STAMP_FLUSH(c, t)
-    if (oq >= 0 && (lane < (t & 63))) out[(int64_t)oq * kmax] = ov;  // last partial group
-    // write the dirty rows back for the next round's scan
-#pragma unroll
-    for (int i = 0; i < UPL; ++i)
-        if (i * 64 + lane < nu) {
-            NodeRec* r = rec + upos[i];
-            r->cpu = ucpu[i];
-            r->mem = umem[i];
-            r->gpu = ugpu[i];
-        }
-    if (lane == 0) res[c] = CommitResult{t, stop, nu, placed};
+    const CommitResult R =
+        commit_window<EPL>(c, P, rec, cand, rank_stride, nranks, bnd, wjob, out, kmax, bitmap);
+    if (threadIdx.x == 0) res[c] = R;
 }
-#undef FIT_COMMIT_STEP
 
 // ------------------------------------------------------------------- prefilter / setup
 // out[] init, component id per job, rejected marks (FIT_REJECTED) — DESIGN.md §3.1.

@@ -1,0 +1,233 @@
+// fit_persistent.hip — the whole placement in ONE launch.
+//
+// Blocks [0, C) are committers: wave 0 of block c owns partition component c; it publishes each
+// round's scan tiles into a device task ring, waits for its per-component done counter, then
+// runs commit_window (fit_common.h) on the results.  Blocks [C, C+W) are scan workers: they
+// claim tiles from the ring in order and run scan_tile.  Components therefore advance at their
+// own pace — no host round trip and no global round barrier — while the scan work of all of
+// them shares the whole chip.
+//
+// Cross-workgroup hand-offs follow cdna_hip_programming.md §6 Guideline 16 (placement-
+// independent, agent scope):
+//   producer: plain stores → every storing wave `s_waitcnt vmcnt(0)` → barrier → one lane
+//             release fence → `s_waitcnt vmcnt(0)` → relaxed agent atomic (counter / granule)
+//   consumer: relaxed agent poll → ONE acquire fence → `s_waitcnt vmcnt(0)` (→ barrier) → plain
+//             loads; plus `s_dcache_inv` because node rows, plans and job rows are read through
+//             the scalar cache, which an acquire fence does not invalidate.
+// Every spin is bounded; a watchdog trip sets ctl->error and drains every block.
+#include <algorithm>
+
+#include "fit_common.h"
+
+namespace fitgpu {
+
+constexpr unsigned QCAP = 1u << 16;  // task ring entries (8-byte {epoch, tile} granules)
+constexpr unsigned SPIN_LIMIT = 1u << 25;
+constexpr unsigned long long TASK_EXIT = ~0ull;
+
+struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
+    unsigned q_tail;   // tiles reserved by committers
+    unsigned pad0[31];
+    unsigned q_head;   // tiles claimed by workers
+    unsigned pad1[31];
+    unsigned finished;  // components done
+    unsigned error;     // 1 = watchdog
+    unsigned pad2[30];
+    unsigned done[32][32];  // per component tiles completed (own 128-B line each)
+};
+
+__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void acquire_agent() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_dcache_inv();  // scalar cache: node rows, plans, job rows are s_loaded
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void release_agent() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
+}
+
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
+    EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
+    const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
+    int ncomp, NodeRec* __restrict__ rec, const int32_t* __restrict__ jl,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk,
+    uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob,
+    int32_t* __restrict__ out, int kmax, int64_t* __restrict__ wbusy) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+
+    if ((int)blockIdx.x < ncomp) {
+        // ================================================================== committer
+        if (threadIdx.x >= 64) return;  // one wave per component
+        const int c = blockIdx.x;
+        const CompState S = cs[c];
+        uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem);
+        int32_t cursor = S.jstart, win = S.wmin;
+        unsigned target = 0;
+        int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
+        while (cursor < S.jend) {
+            const int w = min(win, S.jend - cursor);
+            CompPlan P;
+            P.nb = S.nb;
+            P.ne = S.ne;
+            P.sb = S.sb;
+            P.se = S.se;
+            P.nslice = S.nslice;
+            P.sub = S.sub;
+            P.jbase = cursor;
+            P.w = w;
+            P.blk0 = 0;
+            P.cand_off = S.cand_off;
+            P.slot0 = S.slot0;
+            if (lane == 0) plans[c] = P;
+            for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+            release_agent();  // plan, bound reset and last round's node rows → visible
+            const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
+            unsigned base = 0;
+            if (lane == 0)
+                base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            base = __builtin_amdgcn_readfirstlane(base);
+            for (unsigned i = lane; i < ntiles; i += 64) {
+                const unsigned idx = base + i;
+                const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
+                const unsigned long long g =
+                    ((unsigned long long)(idx / QCAP + 1) << 32) | (tile << 10) | (sl << 6) | c;
+                __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            target += ntiles;
+            const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            unsigned spins = 0;
+            bool fail = false;
+            while (ld_agent(&ctl->done[c][0]) < target) {
+                if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) {
+                    fail = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (fail) {
+                if (lane == 0) atomicOr(&ctl->error, 1u);
+                break;
+            }
+            acquire_agent();  // candidates, bounds, window job rows of this round
+            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            const CommitResult R =
+                commit_window<1>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
+            const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            tw += t1 - t0;
+            tc += t2 - t1;
+            evals += (int64_t)w * (S.se - S.sb);
+            placed += R.placed;
+            ++rounds;
+            sr += R.stop == 1;
+            sd += R.stop == 2;
+            cursor += R.done;
+            const int nw = R.stop ? 2 * R.done : 2 * w;
+            win = max(S.wmin, min(S.wmax, nw));
+        }
+        release_agent();  // last round's node rows / placements (kernel end also flushes)
+        if (lane == 0) {
+            co[c] = CompOut{evals, placed, cursor - S.jstart, rounds, sr, sd, tc, tw};
+            __hip_atomic_fetch_add(&ctl->finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+
+    // ====================================================================== scan worker
+    uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
+    unsigned long long* task_slot =
+        reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
+    int64_t busy = 0;  // realtime ticks (100 MHz) spent scanning
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
+            unsigned long long task = TASK_EXIT;
+            for (unsigned spins = 0;; ++spins) {
+                const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
+                                                               __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                if ((g >> 32) == want) {
+                    task = g;
+                    break;
+                }
+                if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
+                if (spins > SPIN_LIMIT) {
+                    atomicOr(&ctl->error, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            *task_slot = task;
+        }
+        __syncthreads();
+        const unsigned long long task = *task_slot;
+        if (task == TASK_EXIT) {  // block-uniform
+            if (threadIdx.x == 0) wbusy[blockIdx.x - ncomp] = busy;
+            return;
+        }
+        const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) acquire_agent();
+        else __builtin_amdgcn_s_dcache_inv();
+        __syncthreads();
+        const int c = (int)(task & 63u);
+        const int s = (int)((task >> 6) & 15u);
+        const int tile = (int)((task >> 10) & 0x3fffffu);
+        const CompPlan P = plans[c];
+        scan_tile<true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,
+                        xk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            release_agent();
+            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
+        }
+        __syncthreads();  // task_slot is rewritten by thread 0 next iteration
+    }
+}
+
+size_t engine_lds_bytes(int32_t max_component_nodes) {
+    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16;
+    const size_t bits = (size_t)((max_component_nodes + 31) / 32) * 4;
+    return std::max(scan, bits);
+}
+
+size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
+size_t engine_ring_bytes() { return sizeof(unsigned long long) * QCAP; }
+
+int engine_blocks_per_cu(size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine, SCAN_WAVES * 64, lds) !=
+        hipSuccess)
+        return 0;
+    return n;
+}
+
+hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
+                         const void* cs, void* co, CompPlan* plans, int ncomp, NodeRec* rec,
+                         const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
+                         const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                         const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
+                         int32_t* out, int kmax, int64_t* wbusy) {
+    hipLaunchKernelGGL(k_engine, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,
+                       static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),
+                       static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,
+                       rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, out, kmax,
+                       wbusy);
+    return hipGetLastError();
+}
+
+}  // namespace fitgpu

@@ -51,7 +51,8 @@ class FitStats(C.Structure):
                 ("rejected", C.c_int64), ("rounds", C.c_int64), ("evals", C.c_int64),
                 ("useful_evals", C.c_int64), ("stops_rescan", C.c_int64),
                 ("stops_dirty", C.c_int64), ("ms_total", C.c_double), ("ms_scan", C.c_double),
-                ("ms_commit", C.c_double), ("ms_exchange", C.c_double), ("shard_mode", C.c_int32),
+                ("ms_commit", C.c_double), ("ms_exchange", C.c_double), ("ms_device", C.c_double),
+                ("shard_mode", C.c_int32),
                 ("components", C.c_int32)]
 
     def as_dict(self):
