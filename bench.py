@@ -36,6 +36,44 @@ def commit_bytes_per_job(entries: int) -> int:
     return entries * 8 + 32 + 8 + 4  # candidate keys + job row + bound + placement
 
 
+def kernel_table(agg, stats, steps, world, evals_local):
+    """Per-kernel live timings (engine HIP events) and their rooflines.
+
+    Persistent engine (engine == 1): ONE k_engine launch per step; its duration is ms_device.  The
+    scan work it contains is VALU-bound (12 int32 ops per performed eval); the serial commit chain
+    inside it is latency-bound and reported as ns per committed job.
+    Host-driven rounds (engine == 0): one k_scan + one k_commit launch per round."""
+    rounds = max(agg["rounds"], 1)
+    jobs_resolved = agg["placed"] + agg["unplaced"]
+    if all(s.get("engine", 0) == 1 for s in stats):
+        ms = agg["ms_device"] / steps
+        ops = evals_local / steps * SCAN_OPS_PER_EVAL
+        tops = ops / (ms * 1e-3) / 1e12
+        return {"k_engine": {
+            "ms_per_launch": round(ms, 4), "launches": steps, "bound": "valu",
+            "achieved": round(tops, 3), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
+            "frac": round(tops / PEAK_VALU_TOPS, 4),
+            "hbm_gbs_algorithmic": round(evals_local / steps * SCAN_BYTES_PER_EVAL / (ms * 1e-3) / 1e9, 1),
+            "scan_worker_busy_ms": round(agg["ms_scan"] / steps, 3),
+            "commit_chain_ms": round(agg["ms_commit"] / steps, 3),
+            "rounds_longest_component": agg["rounds"] / steps}}
+    scan_ms = agg["ms_scan"] / rounds
+    commit_ms = agg["ms_commit"] / rounds
+    evals_per_launch = evals_local / rounds
+    scan_tops = evals_per_launch * SCAN_OPS_PER_EVAL / (scan_ms * 1e-3) / 1e12
+    entries = 64 * (world if stats[-1]["shard_mode"] == 1 else 1)
+    commit_gbs = jobs_resolved / rounds * commit_bytes_per_job(entries) / (commit_ms * 1e-3) / 1e9
+    return {
+        "k_scan": {"ms_per_launch": round(scan_ms, 4), "launches": rounds, "bound": "valu",
+                   "achieved": round(scan_tops, 3), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
+                   "frac": round(scan_tops / PEAK_VALU_TOPS, 4),
+                   "hbm_gbs_algorithmic": round(evals_per_launch * SCAN_BYTES_PER_EVAL / (scan_ms * 1e-3) / 1e9, 1)},
+        "k_commit": {"ms_per_launch": round(commit_ms, 4), "launches": rounds, "bound": "latency",
+                     "achieved": round(commit_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(commit_gbs / PEAK_HBM_GBS, 5)},
+    }
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,8 +152,8 @@ def main():
     assert s0["placed"] + s0["unplaced"] + s0["rejected"] == jobs.j
 
     value = jobs.j * a.steps / el
-    agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan",
-                                                  "ms_commit", "ms_exchange", "placed", "unplaced")}
+    agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan", "ms_commit",
+                                                  "ms_exchange", "ms_device", "placed", "unplaced")}
     evals_local = agg["evals"]
     if world > 1:  # performed evaluations summed over ranks (each rank scanned its own share)
         t = torch.tensor([float(agg["evals"])], dtype=torch.float64, device=dev)
@@ -123,25 +161,8 @@ def main():
         agg["evals"] = int(t.item())
     used_mode = {0: "1 GPU", 1: f"node-sharded x{world} (RCCL allgather + u64 min-allreduce per round)",
                  2: f"partition-component-sharded x{world} (one RCCL merge)"}[stats[-1]["shard_mode"]]
-    rounds = max(agg["rounds"], 1)
-    scan_ms = agg["ms_scan"] / rounds
-    commit_ms = agg["ms_commit"] / rounds
-    evals_per_launch = evals_local / rounds
-    scan_tops = evals_per_launch * SCAN_OPS_PER_EVAL / (scan_ms * 1e-3) / 1e12
-    # commit: one launch per round resolves (placed+unplaced in window) jobs; bytes model DESIGN §5
-    entries = 64 * (world if stats[-1]["shard_mode"] == 1 else 1)
-    commit_jobs = (agg["placed"] + agg["unplaced"]) / rounds
-    commit_gbs = commit_jobs * commit_bytes_per_job(entries) / (commit_ms * 1e-3) / 1e9
-    kernels = {
-        "fit_scan": {"ms_per_launch": round(scan_ms, 4), "launches": rounds, "bound": "valu",
-                     "achieved": round(scan_tops, 3), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
-                     "frac": round(scan_tops / PEAK_VALU_TOPS, 4),
-                     "hbm_gbs_algorithmic": round(evals_per_launch * SCAN_BYTES_PER_EVAL / (scan_ms * 1e-3) / 1e9, 1)},
-        "fit_commit": {"ms_per_launch": round(commit_ms, 4), "launches": rounds, "bound": "latency",
-                       "achieved": round(commit_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                       "frac": round(commit_gbs / PEAK_HBM_GBS, 5)},
-    }
-    dominant = "fit_scan" if agg["ms_scan"] >= agg["ms_commit"] else "fit_commit"
+    kernels = kernel_table(agg, stats, a.steps, world, evals_local)
+    dominant = max(kernels, key=lambda k: kernels[k]["ms_per_launch"] * kernels[k]["launches"])
     k = kernels[dominant]
     traffic = None
     if a.pmc_json and os.path.exists(a.pmc_json):

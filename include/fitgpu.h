@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 1
+#define FITGPU_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -95,6 +95,8 @@ typedef struct {
     double ms_device;      /* device time of the placement launches (HIP events)             */
     int32_t shard_mode;    /* mode used (FIT_SHARD_NODES / FIT_SHARD_COMPONENTS; 0 if world 1) */
     int32_t components;    /* independent partition components                               */
+    int32_t engine;        /* 1: persistent single-launch engine (k_engine); 0: host-driven rounds */
+    int32_t reserved;
 } fit_stats;
 
 /* ---- engine -------------------------------------------------------------------------- */

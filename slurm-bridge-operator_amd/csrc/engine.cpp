@@ -383,10 +383,12 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     const size_t lds = engine_lds_bytes(maxnodes);
     int per_cu = engine_blocks_per_cu(lds);
     if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine does not fit on a CU (lds %zu)", lds);
-    // every block must be resident (workers and committers spin on each other): stay one block
-    // per CU below the occupancy answer (it can over-report by one; MI355X_MICROARCH.md)
-    const int resident = std::max(1, per_cu - 1) * c->cus;
-    const int workers = std::max(8, resident - nc);
+    // Only the committers (blocks [0, nc), dispatched first) must be co-resident: a worker block
+    // that is not yet resident has claimed no task, so nobody waits on it.  One block per CU:
+    // the scan workers are mostly idle already, and a second block on a committer's CU slows
+    // the serial commit chain (measured: 2/CU → commit +3%, no scan gain).
+    int workers = std::max(8, std::max(1, per_cu - 1) * c->cus - nc);
+    if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
     if (c->ebusy.ensure(workers) || c->h_ebusy.ensure(workers)) return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
@@ -497,6 +499,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     if (c->persistent && !node_sharded) {
         int rc = run_persistent(c, jb, owned, cpu, mem, gpu, wall, part, nk, out, kmax, S);
         if (rc) return rc;
+        S.engine = 1;
     } else {
     std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
     if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||

@@ -1,0 +1,485 @@
+// fit_commit_mw.h — the commit of one component's window by a whole 8-wave workgroup
+// (DESIGN.md §3.7): one DECIDER wave walks the jobs in priority order; seven HELPER waves
+// pre-resolve the jobs ahead of it against a slightly stale snapshot of the dirty state.
+//
+// Why it is exact.  Let the decider have resolved jobs [0, v) when a helper snapshots the
+// state for job t (v >= t - (MW_M - 1), enforced by the helper).  The helper records the MW_M
+// smallest keys <= B among (clean candidates of t) ∪ (dirty rows), each item tagged clean (with
+// its node row) or dirty (its slot).  When the decider reaches t, only the nodes written by jobs
+// [v, t) — at most MW_M - 1 of them, the decider's own last decisions — can differ from the
+// snapshot.  It drops every listed item whose node is among them (a clean node since marked in
+// the bitmap, a dirty slot whose version is >= v) and re-evaluates those nodes at their current
+// state.  If the list held MW_M items, at least one survives and every unlisted node has a key
+// above it; if it held fewer, it held every candidate <= B.  Either way
+//     best = min(surviving items, re-evaluated nodes)
+// is the sequential answer restricted to keys <= B, and the SPEC stop rule reduces to
+// "best > B with B finite" (a clean candidate is always <= B).  No fallback path exists.
+//
+// LDS protocol (one workgroup): DS instructions of a wave execute in issue order, so plain
+// stores followed by a flag store are seen in that order by a wave that read the flag first;
+// the fences below are compiler barriers only.
+#pragma once
+#include "fit_common.h"
+
+namespace fitgpu {
+
+constexpr int MW_M = 8;                 // items per pre-resolved record (> snapshot lag)
+constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once job t-8 is decided
+constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
+#ifndef MW_HELPERS
+#define MW_HELPERS 7
+#endif
+constexpr int MW_H = MW_HELPERS;  // 6: wave 4 (the decider's SIMD partner) stays idle
+constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
+#ifndef MW_HSLEEP
+#define MW_HSLEEP 2
+#endif
+static_assert(MAX_SLICES * KS <= 64, "one candidate entry per lane");
+static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
+
+struct alignas(16) MwRow {  // dirty row, current state
+    int32_t cpu, mem, gpu, avail;
+    uint32_t mask, pos;
+    int32_t orig, ver;  // ver: last job (window index) that created or changed it
+};
+
+struct alignas(16) MwItem {
+    uint64_t key;
+    int32_t tag;   // >= 0 dirty slot; -1 clean candidate (row below)
+    int32_t orig;
+    int32_t cpu, mem, gpu, avail;
+    uint32_t mask, pad0, pad1, pad2;
+};
+
+struct alignas(16) MwHdr {
+    uint32_t ready;  // t + 1 once the record of job t is complete
+    int32_t v, n, q;
+    int32_t cpu, mem, gpu, wall;
+    uint32_t pbit, pad;
+    uint64_t B;
+};
+
+struct alignas(16) MwRec {
+    MwHdr h;
+    MwItem it[MW_M];
+};
+
+struct alignas(16) MwShared {
+    uint32_t decided;  // jobs resolved by the decider
+    uint32_t nu;       // dirty rows (stored together with decided)
+    uint32_t halt;     // decider stopped early
+    uint32_t fail;     // helper / decider watchdog
+    int32_t res[4];    // CommitResult of the window
+    uint32_t pad[8];
+    MwRec rec[MW_R];
+    MwRow rows[UCAP];
+    uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
+};
+
+__host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
+    return sizeof(MwShared) + (size_t)((max_component_nodes + 31) / 32) * 4;
+}
+
+#ifdef FIT_STAMPS
+// [comp][0] decider cycles, [1] decider wait-for-record, [2] decided jobs,
+// [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
+// [7] decider check+reduce, [8] decider decide+publish
+__device__ unsigned long long g_mw[64][16];
+#define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MW_DECL(v) unsigned long long v = 0
+#define MW_ACC(v, x) v += (x)
+#define MW_ADD(I_, V_) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_mw[blockIdx.x & 63][I_], (unsigned long long)(V_)); } while (0)
+#else
+#define MW_CLK(v)
+#define MW_DECL(v)
+#define MW_ACC(v, x)
+#define MW_ADD(I_, V_)
+#endif
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void cbar() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
+
+// a VGPR zero the compiler cannot see through: keeps uniform loads of data written by other
+// workgroups in this launch on the vector path (vmcnt, in order) instead of the scalar cache
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
+__device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, int32_t av,
+                                           uint32_t mask, uint32_t pos, int32_t jc, int32_t jm,
+                                           int32_t jg, int32_t jw, uint32_t jp) {
+    const int32_t dc = cf - jc, dm = mf - jm, dg = gf - jg, da = av - jw;
+    const bool ok = (dc | dm | dg | da) >= 0 && (mask & jp);
+    const uint32_t sc = (min((uint32_t)dg, 255u) << 24) | (min((uint32_t)dc, 4095u) << 12) |
+                        min((uint32_t)dm >> 10, 4095u);
+    return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
+}
+
+// ------------------------------------------------------------------------------- helper
+// Helper h (1..MW_H) pre-resolves jobs t = h-1, h-1+MW_H, ...  Loads run two jobs ahead (keys,
+// job row, bound) and one job ahead (the node rows of the candidates); the three register sets
+// are indexed by literal constants only (3-way unrolled loop).
+#define MW_HSTEP(A, B_, C)                                                                     \
+    {                                                                                          \
+        if (t >= P.w) goto hdone;                                                              \
+        { /* node rows of job t+H's candidates (keys arrived last step) */                     \
+            const uint64_t k_ = kk[B_];                                                        \
+            const uint32_t p_ = k_ != KEY_INF ? (uint32_t)k_ : (uint32_t)P.nb;                 \
+            const NodeRec r_ = rec[p_];                                                        \
+            rc[B_] = r_.cpu;                                                                   \
+            rm[B_] = r_.mem;                                                                   \
+            rg[B_] = r_.gpu;                                                                   \
+            ra[B_] = r_.avail;                                                                 \
+            rk[B_] = r_.mask;                                                                  \
+            ro[B_] = r_.orig;                                                                  \
+        }                                                                                      \
+        {                                                                                      \
+            const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
+            kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                             \
+            jr[C] = wjob[P.slot0 + tt_];                                                       \
+            jbd[C] = bnd[P.slot0 + tt_];                                                       \
+        }                                                                                      \
+        /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs */                  \
+        uint32_t v_;                                                                           \
+        MW_CLK(hw0_);                                                                          \
+        for (unsigned sp_ = 0;; ++sp_) {                                                       \
+            v_ = lds_ld(&S->decided);                                                          \
+            if ((int)v_ + (MW_M - 1) >= t) break;                                              \
+            if (lds_ld(&S->halt) | lds_ld(&S->fail)) goto hdone;                               \
+            if (sp_ > MW_SPIN_LIMIT) {                                                         \
+                lds_st(&S->fail, 1u);                                                          \
+                goto hdone;                                                                    \
+            }                                                                                  \
+            __builtin_amdgcn_s_sleep(MW_HSLEEP); /* keep the LDS free for the decider */       \
+        }                                                                                      \
+        cbar();                                                                                \
+        {                                                                                      \
+            MW_CLK(hw1_);                                                                      \
+            MW_ACC(a_hw, hw1_ - hw0_);                                                         \
+        }                                                                                      \
+        const int nu_ = (int)lds_ld(&S->nu);                                                   \
+        const JobRec& J_ = jr[A];                                                              \
+        const uint64_t Bd_ = jbd[A];                                                           \
+        uint64_t x0;                                                                           \
+        {                                                                                      \
+            const uint64_t k_ = kk[A];                                                         \
+            const bool ok_ = k_ <= Bd_ && k_ != KEY_INF;                                       \
+            const uint32_t rel_ = ok_ ? (uint32_t)k_ - (uint32_t)P.nb : 0u;                    \
+            const bool dirty_ = (S->bitmap[rel_ >> 5] >> (rel_ & 31)) & 1u;                    \
+            x0 = ok_ && !dirty_ ? k_ : KEY_INF;                                                \
+        }                                                                                      \
+        uint64_t xd[UPL];                                                                      \
+        MwRow wr_[UPL];                                                                        \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) {                                      \
+            xd[i] = KEY_INF;                                                                   \
+            const int u_ = i * 64 + lane;                                                      \
+            if (i * 64 < nu_) {                                                                \
+                wr_[i] = S->rows[u_ < nu_ ? u_ : 0];                                           \
+                const uint64_t y_ = mw_key(wr_[i].cpu, wr_[i].mem, wr_[i].gpu, wr_[i].avail,   \
+                                           wr_[i].mask, wr_[i].pos, J_.cpu, J_.mem, J_.gpu,    \
+                                           J_.wall, J_.pbit);                                  \
+                xd[i] = u_ < nu_ && y_ <= Bd_ ? y_ : KEY_INF;                                  \
+            }                                                                                  \
+        }                                                                                      \
+        MwRec* R_ = &S->rec[t & (MW_R - 1)];                                                   \
+        int n_ = 0;                                                                            \
+        /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */ \
+        const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
+        for (; n_ < nmax_; ++n_) {                                                             \
+            uint64_t h_ = x0;                                                                  \
+            _Pragma("unroll") for (int i = 0; i < UPL; ++i) h_ = umin64(h_, xd[i]);            \
+            const uint64_t best_ = wave_min_key(h_);                                           \
+            if (best_ == KEY_INF) break;                                                       \
+            const int w_ = __builtin_ctzll(__ballot(h_ == best_));                             \
+            if (lane == w_) {                                                                  \
+                MwItem* it_ = &R_->it[n_];                                                     \
+                if (x0 == best_) {                                                             \
+                    *it_ = MwItem{best_, -1, ro[A], rc[A], rm[A], rg[A], ra[A], rk[A], 0, 0, 0}; \
+                    x0 = KEY_INF;                                                              \
+                } else {                                                                       \
+                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (xd[i] == best_) {      \
+                        *it_ = MwItem{best_, i * 64 + lane, wr_[i].orig, wr_[i].cpu,           \
+                                      wr_[i].mem, wr_[i].gpu, wr_[i].avail, wr_[i].mask,       \
+                                      0, 0, 0};                                                \
+                        xd[i] = KEY_INF;                                                       \
+                    }                                                                          \
+                }                                                                              \
+            }                                                                                  \
+        }                                                                                      \
+        if (lane == 0) {                                                                       \
+            R_->h.v = (int32_t)v_;                                                             \
+            R_->h.n = n_;                                                                      \
+            R_->h.q = J_.q;                                                                    \
+            R_->h.cpu = J_.cpu;                                                                \
+            R_->h.mem = J_.mem;                                                                \
+            R_->h.gpu = J_.gpu;                                                                \
+            R_->h.wall = J_.wall;                                                              \
+            R_->h.pbit = J_.pbit;                                                              \
+            R_->h.B = Bd_;                                                                     \
+            cbar();                                                                            \
+            lds_st(&R_->h.ready, (uint32_t)t + 1u);                                            \
+        }                                                                                      \
+        MW_ACC(a_hn, 1);                                                                       \
+        MW_ACC(a_hi, n_);                                                                      \
+        t += MW_H;                                                                             \
+    }
+
+__device__ __forceinline__ void mw_helper(const CompPlan& P, MwShared* S,
+                                          const NodeRec* __restrict__ rec,
+                                          const uint64_t* __restrict__ cand,
+                                          const uint64_t* __restrict__ bnd,
+                                          const JobRec* __restrict__ wjob, int h) {
+    const int lane = threadIdx.x & 63;
+    const int E = P.nslice * KS;
+    const bool has = lane < E;
+    const int64_t eoff = P.cand_off + (has ? lane : 0);
+    const int wlast = P.w - 1;
+    const int z = opaque_zero();
+    int t = h - 1;
+
+    uint64_t kk[3], jbd[3];
+    JobRec jr[3];
+    int32_t rc[3], rm[3], rg[3], ra[3], ro[3];
+    uint32_t rk[3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // jobs t and t + H
+        const int tt = min(t + s * MW_H, wlast) + z;
+        kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
+        jr[s] = wjob[P.slot0 + tt];
+        jbd[s] = bnd[P.slot0 + tt];
+    }
+    {
+        const uint32_t p = kk[0] != KEY_INF ? (uint32_t)kk[0] : (uint32_t)P.nb;
+        const NodeRec r = rec[p];
+        rc[0] = r.cpu;
+        rm[0] = r.mem;
+        rg[0] = r.gpu;
+        ra[0] = r.avail;
+        rk[0] = r.mask;
+        ro[0] = r.orig;
+    }
+    MW_DECL(a_hw);
+    MW_DECL(a_hn);
+    MW_DECL(a_hi);
+    MW_CLK(h0);
+    for (;;) {
+        MW_HSTEP(0, 1, 2)
+        MW_HSTEP(1, 2, 0)
+        MW_HSTEP(2, 0, 1)
+    }
+hdone:;
+    MW_CLK(h1);
+    MW_ADD(3, h1 - h0);
+    MW_ADD(4, a_hw);
+    MW_ADD(5, a_hn);
+    MW_ADD(6, a_hi);
+}
+#undef MW_HSTEP
+
+// ------------------------------------------------------------------------------ decider
+// The "written ring": lane l (and every lane l + 8k) holds the row the decider wrote for the
+// last job j ≡ l (mod 8): job index, slot and the row's current fields.  For job t an entry is
+// live iff its job >= v (the record's snapshot); live entries are exactly the nodes that may
+// differ from the snapshot, so they are re-evaluated and every record item on one of their
+// positions is dropped.  When a slot is written again its older entry dies (job = -1), so a live
+// entry always holds the slot's current row.  All decision work is VALU on lanes 0..7; the only
+// LDS round trip per job is the record read.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_rot(uint32_t v) {  // within a 16-lane row, all valid
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_min8(uint32_t v) { return min(v, dpp_rot<CTRL>(v)); }
+
+// min over lanes 0..7 (valid in every one of them): quad swaps, then half-row mirror
+__device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
+    v = dpp_min8<0xb1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_min8<0x4e>(v);   // quad_perm [2,3,0,1]
+    v = dpp_min8<0x141>(v);  // row_half_mirror
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+}
+
+__device__ __forceinline__ CommitResult mw_decider(const CompPlan& P, MwShared* S,
+                                                   int32_t* __restrict__ out, int kmax) {
+    const int lane = threadIdx.x & 63;
+    const int l8 = lane & 7;
+    const uint32_t nb = (uint32_t)P.nb;
+#ifndef MW_NO_SETPRIO
+    __builtin_amdgcn_s_setprio(3);  // shares its SIMD with helper wave 4
+#endif
+    int nu = 0, placed = 0, stop = 0, t = 0;
+    int32_t wj = -1, ws = -1, wc = 0, wm = 0, wg = 0, wa = 0, wo = -1;  // written ring
+    uint32_t wk = 0, wp = ~0u;
+    int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
+    MW_DECL(a_dw);
+    MW_DECL(a_dc);
+    MW_DECL(a_dd);
+    MW_CLK(d0);
+    for (; t < P.w; ++t) {
+        MwRec* R = &S->rec[t & (MW_R - 1)];
+        MW_CLK(dw0);
+        MwHdr h;
+        MwItem it;
+        for (unsigned sp = 0;; ++sp) {  // speculative: ready, header and items in one round trip
+            const uint32_t rd = lds_ld(&R->h.ready);
+            cbar();
+            h = R->h;
+            it = R->it[l8];
+#ifdef MW_DECIDER_BENCH
+            if (true) break;  // diagnostic: records pre-filled, no helpers
+#endif
+            if (rd == (uint32_t)t + 1u) break;
+            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
+                lds_st(&S->fail, 1u);
+                stop = 3;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(0);
+        }
+        if (stop) break;
+        MW_CLK(dw1);
+        MW_ACC(a_dw, dw1 - dw0);
+        const bool live = wj >= h.v;
+        const uint32_t lp = live ? wp : ~0u;
+        const uint32_t ip = (uint32_t)it.key;
+        bool hit = ip == lp;
+        hit |= ip == dpp_rot<0x121>(lp);  // row_ror:1..7 (lanes 8..15 mirror 0..7)
+        hit |= ip == dpp_rot<0x122>(lp);
+        hit |= ip == dpp_rot<0x123>(lp);
+        hit |= ip == dpp_rot<0x124>(lp);
+        hit |= ip == dpp_rot<0x125>(lp);
+        hit |= ip == dpp_rot<0x126>(lp);
+        hit |= ip == dpp_rot<0x127>(lp);
+        const uint64_t ival = lane < h.n && !hit ? it.key : KEY_INF;
+        const uint64_t wkey =
+            live && lane < 8 ? mw_key(wc, wm, wg, wa, wk, wp, h.cpu, h.mem, h.gpu, h.wall, h.pbit)
+                             : KEY_INF;
+        const uint64_t val = umin64(ival, wkey);
+        const uint32_t mh = min8_u32((uint32_t)(val >> 32));
+        const uint32_t ml = min8_u32((uint32_t)(val >> 32) == mh ? (uint32_t)val : ~0u);
+        const uint64_t best = ((uint64_t)mh << 32) | ml;
+        MW_CLK(dw2);
+        MW_ACC(a_dc, dw2 - dw1);
+        // one straight-line decision; the only exit is the (rare, uniform) stop
+        const bool any = best != KEY_INF;
+        const int w = __builtin_ctzll(__ballot(val == best) | (1ull << 63));
+        const bool fi = ival == best;  // the winner is a record item (else a ring row)
+        int32_t slot = __builtin_amdgcn_readlane(fi ? it.tag : ws, w);
+        const bool fresh = any && slot < 0;  // a clean node becomes dirty row nu
+        const bool s1 = __ballot(h.B != KEY_INF && best > h.B) != 0;
+        if (s1 || (fresh && nu == UCAP)) {
+            stop = s1 ? 1 : 2;  // 1: candidate list exhausted (rescan); 2: dirty set full
+            break;
+        }
+        int32_t node = -1;
+        if (any) {
+            slot = fresh ? nu : slot;
+            nu += fresh;
+            ++placed;
+            const int32_t nc = __builtin_amdgcn_readlane((fi ? it.cpu : wc) - h.cpu, w);
+            const int32_t nm = __builtin_amdgcn_readlane((fi ? it.mem : wm) - h.mem, w);
+            const int32_t ng = __builtin_amdgcn_readlane((fi ? it.gpu : wg) - h.gpu, w);
+            const int32_t na = __builtin_amdgcn_readlane(fi ? it.avail : wa, w);
+            const uint32_t nk = __builtin_amdgcn_readlane(fi ? it.mask : wk, w);
+            node = __builtin_amdgcn_readlane(fi ? it.orig : wo, w);
+            if (lane == 0) {
+                S->rows[slot] = MwRow{nc, nm, ng, na, nk, ml, node, t};
+                if (fresh) {
+                    const uint32_t rel = ml - nb;
+                    __hip_atomic_fetch_or(&S->bitmap[rel >> 5], 1u << (rel & 31),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            // ring: the entry of job t; an older entry of the same slot dies
+            const bool me = l8 == (t & 7);
+            wj = me ? t : (ws == slot ? -1 : wj);
+            ws = me ? slot : ws;
+            wc = me ? nc : wc;
+            wm = me ? nm : wm;
+            wg = me ? ng : wg;
+            wa = me ? na : wa;
+            wk = me ? nk : wk;
+            wp = me ? ml : wp;
+            wo = me ? node : wo;
+        }
+        if (lane == (t & 63)) {
+            oq = h.q;
+            ov = node;
+        }
+        if ((t & 63) == 63) {  // uniform: flush 64 placements
+            if (oq >= 0) out[(int64_t)oq * kmax] = ov;
+            oq = -1;
+        }
+        cbar();
+        if (lane == 0)  // {decided, nu} in one 8-byte LDS store
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
+                               ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        MW_CLK(dw3);
+        MW_ACC(a_dd, dw3 - dw2);
+    }
+    if (oq >= 0 && lane < (t & 63)) out[(int64_t)oq * kmax] = ov;  // last partial group
+    if (stop) lds_st(&S->halt, 1u);
+    MW_CLK(d1);
+    MW_ADD(0, d1 - d0);
+    MW_ADD(2, t);
+    MW_ADD(1, a_dw);
+    MW_ADD(7, a_dc);
+    MW_ADD(8, a_dd);
+    return CommitResult{t, stop, nu, placed};
+}
+
+// All MW_WAVES waves of the block call this; returns the same result in every wave.
+__device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwShared* S,
+                                                         NodeRec* __restrict__ rec,
+                                                         const uint64_t* __restrict__ cand,
+                                                         const uint64_t* __restrict__ bnd,
+                                                         const JobRec* __restrict__ wjob,
+                                                         int32_t* __restrict__ out, int kmax) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nwords = (P.ne - P.nb + 31) >> 5;
+    for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
+    if (threadIdx.x < MW_R) S->rec[threadIdx.x].h.ready = 0u;
+    if (threadIdx.x == 0) {
+        S->decided = 0u;
+        S->halt = 0u;
+        S->nu = 0u;
+        S->fail = 0u;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const CommitResult r = mw_decider(P, S, out, kmax);
+        if (threadIdx.x == 0) {
+            S->res[0] = r.done;
+            S->res[1] = r.stop;
+            S->res[2] = r.dirty;
+            S->res[3] = r.placed;
+        }
+    } else if (MW_H == MW_WAVES - 1) {
+        mw_helper(P, S, rec, cand, bnd, wjob, wave);
+    } else if (wave != 4) {
+        mw_helper(P, S, rec, cand, bnd, wjob, wave < 4 ? wave : wave - 1);
+    }
+    __syncthreads();
+    const CommitResult r{S->res[0], S->res[1], S->res[2], S->res[3]};
+    // write the dirty rows back for the next round's scan
+    for (int u = threadIdx.x; u < r.dirty; u += MW_WAVES * 64) {
+        const MwRow w = S->rows[u];
+        NodeRec* d = rec + w.pos;
+        d->cpu = w.cpu;
+        d->mem = w.mem;
+        d->gpu = w.gpu;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+    __syncthreads();
+    return r;
+}
+
+}  // namespace fitgpu

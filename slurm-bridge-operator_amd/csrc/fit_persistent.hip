@@ -17,7 +17,7 @@
 // Every spin is bounded; a watchdog trip sets ctl->error and drains every block.
 #include <algorithm>
 
-#include "fit_common.h"
+#include "fit_commit_mw.h"
 
 namespace fitgpu {
 
@@ -67,10 +67,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
 
     if ((int)blockIdx.x < ncomp) {
         // ================================================================== committer
-        if (threadIdx.x >= 64) return;  // one wave per component
+        // Wave 0 runs the round protocol (publish tiles, wait, acquire); then all 8 waves commit
+        // the window together: wave 0 decides, waves 1..7 pre-resolve (fit_commit_mw.h).
+        __shared__ int s_fail;
+        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int c = blockIdx.x;
         const CompState S = cs[c];
-        uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem);
+        MwShared* M = reinterpret_cast<MwShared*>(smem);
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target = 0;
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
@@ -88,42 +91,48 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             P.blk0 = 0;
             P.cand_off = S.cand_off;
             P.slot0 = S.slot0;
-            if (lane == 0) plans[c] = P;
-            for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
-            release_agent();  // plan, bound reset and last round's node rows → visible
-            const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
-            unsigned base = 0;
-            if (lane == 0)
-                base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-            base = __builtin_amdgcn_readfirstlane(base);
-            for (unsigned i = lane; i < ntiles; i += 64) {
-                const unsigned idx = base + i;
-                const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
-                const unsigned long long g =
-                    ((unsigned long long)(idx / QCAP + 1) << 32) | (tile << 10) | (sl << 6) | c;
-                __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            target += ntiles;
-            const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            unsigned spins = 0;
-            bool fail = false;
-            while (ld_agent(&ctl->done[c][0]) < target) {
-                if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) {
-                    fail = true;
-                    break;
+            int64_t t0 = 0;
+            if (wave == 0) {
+                if (lane == 0) plans[c] = P;
+                for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+                release_agent();  // plan, bound reset and last round's node rows → visible
+                const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
+                unsigned base = 0;
+                if (lane == 0)
+                    base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                base = __builtin_amdgcn_readfirstlane(base);
+                for (unsigned i = lane; i < ntiles; i += 64) {
+                    const unsigned idx = base + i;
+                    const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
+                    const unsigned long long g = ((unsigned long long)(idx / QCAP + 1) << 32) |
+                                                 (tile << 10) | (sl << 6) | c;
+                    __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                target += ntiles;
+                t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                unsigned spins = 0;
+                bool fail = false;
+                while (ld_agent(&ctl->done[c][0]) < target) {
+                    if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) {
+                        fail = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (fail && lane == 0) atomicOr(&ctl->error, 1u);
+                acquire_agent();  // candidates, bounds, window job rows of this round (CU-wide)
+                if (lane == 0) s_fail = fail;
             }
-            if (fail) {
-                if (lane == 0) atomicOr(&ctl->error, 1u);
+            __syncthreads();
+            if (s_fail) break;  // block-uniform
+            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            const CommitResult R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax);
+            if (R.stop == 3) {  // commit watchdog
+                if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
                 break;
             }
-            acquire_agent();  // candidates, bounds, window job rows of this round
-            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            const CommitResult R =
-                commit_window<1>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
             tw += t1 - t0;
             tc += t2 - t1;
@@ -136,6 +145,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             const int nw = R.stop ? 2 * R.done : 2 * w;
             win = max(S.wmin, min(S.wmax, nw));
         }
+        if (wave != 0) return;
         release_agent();  // last round's node rows / placements (kernel end also flushes)
         if (lane == 0) {
             co[c] = CompOut{evals, placed, cursor - S.jstart, rounds, sr, sd, tc, tw};
@@ -201,8 +211,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
 
 size_t engine_lds_bytes(int32_t max_component_nodes) {
     const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16;
-    const size_t bits = (size_t)((max_component_nodes + 31) / 32) * 4;
-    return std::max(scan, bits);
+    return std::max(scan, mw_lds_bytes(max_component_nodes));
 }
 
 size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
@@ -231,3 +240,10 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
 }
 
 }  // namespace fitgpu
+
+#ifdef FIT_STAMPS
+extern "C" int fit_debug_mw_stamps(unsigned long long* out /* 64 x 16 */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fitgpu::g_mw), sizeof(fitgpu::g_mw)) == hipSuccess
+               ? 0 : -2;
+}
+#endif

@@ -53,7 +53,7 @@ class FitStats(C.Structure):
                 ("stops_dirty", C.c_int64), ("ms_total", C.c_double), ("ms_scan", C.c_double),
                 ("ms_commit", C.c_double), ("ms_exchange", C.c_double), ("ms_device", C.c_double),
                 ("shard_mode", C.c_int32),
-                ("components", C.c_int32)]
+                ("components", C.c_int32), ("engine", C.c_int32), ("reserved", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,0 +1,31 @@
+"""Diagnostic: decider / helper cycle split of the multi-wave commit (FIT_STAMPS build; dev tool)."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "slurm-bridge-operator_amd")]
+from fitgpu import _lib  # noqa: E402
+_lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", "libfitgpu_stamps.so")
+from fitgpu import Engine, synth  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "c3"
+nodes, jobs, parts = synth.make_config(name)
+with Engine() as e:
+    e.load_nodes(nodes)
+    e.load_partitions(parts)
+    out, st = e.place(jobs)
+    buf = (C.c_ulonglong * (64 * 16))()
+    assert _lib.lib().fit_debug_mw_stamps(buf) == 0
+print({k: st[k] for k in ("ms_total", "ms_commit", "ms_device", "rounds")})
+tot = [sum(buf[c * 16 + i] for c in range(64)) for i in range(16)]
+dj, hj = max(tot[2], 1), max(tot[5], 1)
+print(f"decider: {tot[0] / dj:.0f} cyc/job, waiting for records {tot[1] / dj:.0f}, check+reduce {tot[7] / dj:.0f}, "
+      f"decide+publish {tot[8] / dj:.0f} cyc/job")
+print(f"helpers: {tot[3] / hj:.0f} cyc/job (per helper), waiting for snapshot {tot[4] / hj:.0f}, "
+      f"items/job {tot[6] / hj:.2f}")
+for c in range(64):
+    r = buf[c * 16:(c + 1) * 16]
+    if r[2]:
+        print(f"  comp {c:2d} jobs {r[2]:6d} dec {r[0] / r[2]:6.0f} wait {r[1] / r[2]:6.0f} | "
+              f"help {r[3] / max(r[5], 1):6.0f} wait {r[4] / max(r[5], 1):6.0f}")

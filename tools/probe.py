@@ -6,6 +6,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "slurm-bridge-operator_amd")]
+if os.environ.get("FIT_LIB"):  # a variant build of the library (dev experiments)
+    from fitgpu import _lib  # noqa: E402
+    _lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", os.environ["FIT_LIB"])
 from fitgpu import Engine, synth  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
