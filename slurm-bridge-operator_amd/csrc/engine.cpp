@@ -31,7 +31,7 @@ hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, N
                          int nranks, const uint64_t* bnd, const JobRec* wjob, int32_t* out,
                          int kmax, CommitResult* res);
 hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* jmem,
-                            const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
+                            const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
                             int32_t nj, int32_t kmax, const int32_t* ptab, int32_t np,
                             int32_t* out, int8_t* jcomp);
 hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
@@ -48,7 +48,7 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
                          const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
-                         int32_t* out, int kmax, int64_t* wbusy);
+                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk);
 }  // namespace fitgpu
 
 using namespace fitgpu;
@@ -185,7 +185,7 @@ struct fit_ctx {
     DBuf<int32_t> d_ptab;
 
     // per-call scratch
-    DBuf<int32_t> jcpu, jmem, jgpu, jwall, out, jl;
+    DBuf<int32_t> jcpu, jmem, jgpu, jwall, out, jl, jpk;
     DBuf<uint16_t> jpart, jk;
     DBuf<int8_t> jcomp;
     DBuf<uint64_t> cand, bnd;
@@ -195,11 +195,11 @@ struct fit_ctx {
     HBuf<CompPlan> h_plan;
     HBuf<CommitResult> h_res;
     HBuf<int8_t> h_jcomp;
-    std::vector<int32_t> h_jl;
+    std::vector<int32_t> h_jl, h_jpk;
 
     ~fit_ctx() {
         for (auto* b : {&col_cpu, &col_mem, &col_gpu, &col_av, &perm, &jcpu, &jmem, &jgpu,
-                        &jwall, &out, &jl})
+                        &jwall, &out, &jl, &jpk})
             b->release();
         rec.release();
         col_mask.release();
@@ -396,7 +396,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     HIP_TRY(hipEventRecord(c->ev[0], st));
     HIP_TRY(launch_engine(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
                           c->plan.p, nc, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
-                          c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p));
+                          c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p, c->jpk.p));
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * workers,
@@ -440,7 +440,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     hipStream_t st = c->st;
     // 1. prefilter: out[] init, FIT_REJECTED, component per job
     if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
-    HIP_TRY(launch_prefilter(st, cpu, mem, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
+    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
                              c->jcomp.p));
     HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -449,22 +449,32 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     std::vector<int32_t> jb(C + 1, 0);
     for (int32_t q = 0; q < J; ++q) {
         int8_t k = c->h_jcomp.p[q];
-        if (k >= 0) jb[k + 1]++;
+        if (k >= 0) jb[(k & 0x3f) + 1]++;
         else if (k == -2) S.rejected++;
+        else if (k == -3) return fail(FIT_E_INVAL, "job %d: negative demand or nodes_k > kmax", q);
     }
     for (int k = 0; k < C; ++k) jb[k + 1] += jb[k];
     const int32_t JA = jb[C];
     c->h_jl.resize(std::max(JA, 1));
+    c->h_jpk.resize(JA + 1);  // multi-node jobs before each list position (persistent engine)
     {
         std::vector<int32_t> f(jb.begin(), jb.end() - 1);
         for (int32_t q = 0; q < J; ++q) {
             int8_t k = c->h_jcomp.p[q];
-            if (k >= 0) c->h_jl[f[k]++] = q;
+            if (k >= 0) {
+                const int32_t at = f[k & 0x3f]++;
+                c->h_jl[at] = q;
+                c->h_jpk[at + 1] = (k & 0x40) ? 1 : 0;
+            }
         }
+        c->h_jpk[0] = 0;
+        for (int32_t i = 0; i < JA; ++i) c->h_jpk[i + 1] += c->h_jpk[i];
     }
-    if (c->jl.ensure(std::max(JA, 1))) return FIT_E_OOM;
+    if (c->jl.ensure(std::max(JA, 1)) || c->jpk.ensure(JA + 1)) return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->jl.p, c->h_jl.data(), sizeof(int32_t) * JA, hipMemcpyHostToDevice,
                            st));
+    HIP_TRY(hipMemcpyAsync(c->jpk.p, c->h_jpk.data(), sizeof(int32_t) * (JA + 1),
+                           hipMemcpyHostToDevice, st));
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
 
     // world > 1: split by components (each rank owns whole components, no per-round exchange)
@@ -776,8 +786,8 @@ static int check_place_args(fit_ctx* c, int32_t j, const void* a, const void* b,
     if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
     if (j < 0 || (j > 0 && (!a || !b || !d || !e || !f || !out)))
         return fail(FIT_E_INVAL, "bad job arrays");
-    if (kmax != 1)
-        return fail(FIT_E_INVAL, "kmax=%d: multi-node jobs are not enabled in this build", kmax);
+    if (kmax < 1 || kmax > FIT_MAX_K)
+        return fail(FIT_E_INVAL, "kmax=%d outside [1, %d]", kmax, FIT_MAX_K);
     return 0;
 }
 

@@ -214,9 +214,6 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
             }                                                                                  \
         }                                                                                      \
         if (lane == 0) {                                                                       \
-            R_->h.v = (int32_t)v_;                                                             \
-            R_->h.n = n_;                                                                      \
-            R_->h.q = J_.q;                                                                    \
             R_->h.cpu = J_.cpu;                                                                \
             R_->h.mem = J_.mem;                                                                \
             R_->h.gpu = J_.gpu;                                                                \
@@ -224,14 +221,16 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
             R_->h.pbit = J_.pbit;                                                              \
             R_->h.B = Bd_;                                                                     \
             cbar();                                                                            \
-            lds_st(&R_->h.ready, (uint32_t)t + 1u);                                            \
+            /* {ready, v, n, q}: one 16-byte store, after everything else of the record */     \
+            *reinterpret_cast<uint4*>(&R_->h) =                                                \
+                make_uint4((uint32_t)t + 1u, v_, (uint32_t)n_, (uint32_t)J_.q);                 \
         }                                                                                      \
         MW_ACC(a_hn, 1);                                                                       \
         MW_ACC(a_hi, n_);                                                                      \
         t += MW_H;                                                                             \
     }
 
-__device__ __forceinline__ void mw_helper(const CompPlan& P, MwShared* S,
+__device__ __noinline__ void mw_helper(const CompPlan& P, MwShared* S,
                                           const NodeRec* __restrict__ rec,
                                           const uint64_t* __restrict__ cand,
                                           const uint64_t* __restrict__ bnd,
@@ -306,10 +305,32 @@ __device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
 }
 
-__device__ __forceinline__ CommitResult mw_decider(const CompPlan& P, MwShared* S,
-                                                   int32_t* __restrict__ out, int kmax) {
+// v_writelane_b32: lane `l` of `old` := SGPR `x` (no clang builtin on this toolchain).  The lane
+// select goes through M0 (one SGPR operand per VALU instruction on gfx9).
+__device__ __forceinline__ int32_t writelane(int32_t x, int l, int32_t old) {
+    int32_t r;
+    asm("v_writelane_b32 %0, %1, m0" : "=v"(r) : "s"(x), "{m0}"(l), "0"(old));
+    return r;
+}
+__device__ __forceinline__ uint32_t writelane(uint32_t x, int l, uint32_t old) {
+    return (uint32_t)writelane((int32_t)x, l, (int32_t)old);
+}
+
+// bit 8i of the result is set iff byte i of m is nonzero
+__device__ __forceinline__ uint64_t any_in_byte(uint64_t m) {
+    m |= m >> 4;
+    m |= m >> 2;
+    m |= m >> 1;
+    return m & 0x0101010101010101ull;
+}
+
+// Out of line (as is mw_helper): called once per round, each gets its own register allocation
+// instead of sharing the persistent kernel's (which otherwise spills SGPRs in this loop).
+__device__ __noinline__ CommitResult mw_decider(const CompPlan& P, MwShared* S,
+                                                int32_t* __restrict__ out, int kmax) {
     const int lane = threadIdx.x & 63;
-    const int l8 = lane & 7;
+    const int r8 = lane & 7;   // ring entry this lane holds (full row in lanes 0..7 only)
+    const int i8 = lane >> 3;  // record item this lane reads: lane 8i + r tests item i vs entry r
     const uint32_t nb = (uint32_t)P.nb;
 #ifndef MW_NO_SETPRIO
     __builtin_amdgcn_s_setprio(3);  // shares its SIMD with helper wave 4
@@ -327,15 +348,22 @@ __device__ __forceinline__ CommitResult mw_decider(const CompPlan& P, MwShared* 
         MW_CLK(dw0);
         MwHdr h;
         MwItem it;
-        for (unsigned sp = 0;; ++sp) {  // speculative: ready, header and items in one round trip
-            const uint32_t rd = lds_ld(&R->h.ready);
-            cbar();
-            h = R->h;
-            it = R->it[l8];
+        for (unsigned sp = 0;; ++sp) {  // speculative: header and items in one round trip
+            // {ready, v, n, q} is one 16-byte LDS store on the helper side (its last); read as one
+            const uint4* hp = reinterpret_cast<const uint4*>(&R->h);
+            const uint4* ip = reinterpret_cast<const uint4*>(&R->it[i8]);
+            const uint4 h0 = hp[0], h1 = hp[1], h2 = hp[2];
+            const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2];
+            h = MwHdr{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
+                      (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
+                      ((uint64_t)h2.w << 32) | h2.z};
+            it = MwItem{((uint64_t)i0.y << 32) | i0.x, (int32_t)i0.z, (int32_t)i0.w,
+                        (int32_t)i1.x, (int32_t)i1.y, (int32_t)i1.z, (int32_t)i1.w,
+                        i2.x, i2.y, i2.z, i2.w};
 #ifdef MW_DECIDER_BENCH
             if (true) break;  // diagnostic: records pre-filled, no helpers
 #endif
-            if (rd == (uint32_t)t + 1u) break;
+            if (__builtin_amdgcn_readfirstlane(h.ready) == (uint32_t)t + 1u) break;
             if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                 lds_st(&S->fail, 1u);
                 stop = 3;
@@ -346,73 +374,97 @@ __device__ __forceinline__ CommitResult mw_decider(const CompPlan& P, MwShared* 
         if (stop) break;
         MW_CLK(dw1);
         MW_ACC(a_dw, dw1 - dw0);
-        const bool live = wj >= h.v;
-        const uint32_t lp = live ? wp : ~0u;
-        const uint32_t ip = (uint32_t)it.key;
-        bool hit = ip == lp;
-        hit |= ip == dpp_rot<0x121>(lp);  // row_ror:1..7 (lanes 8..15 mirror 0..7)
-        hit |= ip == dpp_rot<0x122>(lp);
-        hit |= ip == dpp_rot<0x123>(lp);
-        hit |= ip == dpp_rot<0x124>(lp);
-        hit |= ip == dpp_rot<0x125>(lp);
-        hit |= ip == dpp_rot<0x126>(lp);
-        hit |= ip == dpp_rot<0x127>(lp);
-        const uint64_t ival = lane < h.n && !hit ? it.key : KEY_INF;
-        const uint64_t wkey =
-            live && lane < 8 ? mw_key(wc, wm, wg, wa, wk, wp, h.cpu, h.mem, h.gpu, h.wall, h.pbit)
-                             : KEY_INF;
-        const uint64_t val = umin64(ival, wkey);
-        const uint32_t mh = min8_u32((uint32_t)(val >> 32));
-        const uint32_t ml = min8_u32((uint32_t)(val >> 32) == mh ? (uint32_t)val : ~0u);
-        const uint64_t best = ((uint64_t)mh << 32) | ml;
+        const int v = __builtin_amdgcn_readfirstlane(h.v);
+        const int n = __builtin_amdgcn_readfirstlane(h.n);
+        const bool live = wj >= v;
+        // first record item whose node no live ring entry touches (items are sorted by key)
+        const uint64_t tm = __ballot(live && (uint32_t)it.key == wp);
+        const uint64_t valid = n >= 8 ? ~0ull : (1ull << (8 * n)) - 1ull;
+        const uint64_t un = valid & 0x0101010101010101ull & ~any_in_byte(tm);
+        const int il = un ? __builtin_ctzll(un) : 0;  // its lane (8 i*)
+        uint64_t best = KEY_INF;
+        if (un)
+            best = ((uint64_t)__builtin_amdgcn_readlane((int)(it.key >> 32), il) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)it.key, il);
+        // live ring rows at their current state: any better than that item?
+        const uint64_t wk0 = mw_key(wc, wm, wg, wa, wk, wp, h.cpu, h.mem, h.gpu, h.wall, h.pbit);
+        const uint64_t wkey = live ? wk0 : KEY_INF;
+        const uint64_t bet = __ballot(wkey < best) & 0xffull;
+        int rl = -1;  // winning ring lane, -1: the item
+        if (bet) {
+            if (__popcll(bet) == 1) {
+                rl = __builtin_ctzll(bet);
+            } else {
+                const uint32_t mh = min8_u32((uint32_t)(wkey >> 32));
+                const uint32_t ml = min8_u32((uint32_t)(wkey >> 32) == mh ? (uint32_t)wkey : ~0u);
+                rl = __builtin_ctzll(__ballot((uint32_t)(wkey >> 32) == mh &&
+                                              (uint32_t)wkey == ml) & 0xffull);
+            }
+            best = ((uint64_t)__builtin_amdgcn_readlane((int)(wkey >> 32), rl) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wkey, rl);
+        }
         MW_CLK(dw2);
         MW_ACC(a_dc, dw2 - dw1);
-        // one straight-line decision; the only exit is the (rare, uniform) stop
-        const bool any = best != KEY_INF;
-        const int w = __builtin_ctzll(__ballot(val == best) | (1ull << 63));
-        const bool fi = ival == best;  // the winner is a record item (else a ring row)
-        int32_t slot = __builtin_amdgcn_readlane(fi ? it.tag : ws, w);
-        const bool fresh = any && slot < 0;  // a clean node becomes dirty row nu
-        const bool s1 = __ballot(h.B != KEY_INF && best > h.B) != 0;
-        if (s1 || (fresh && nu == UCAP)) {
-            stop = s1 ? 1 : 2;  // 1: candidate list exhausted (rescan); 2: dirty set full
+        if (__ballot(h.B != KEY_INF && best > h.B)) {  // uniform
+            stop = 1;  // candidate list exhausted: rescan next round
             break;
         }
         int32_t node = -1;
-        if (any) {
-            slot = fresh ? nu : slot;
-            nu += fresh;
-            ++placed;
-            const int32_t nc = __builtin_amdgcn_readlane((fi ? it.cpu : wc) - h.cpu, w);
-            const int32_t nm = __builtin_amdgcn_readlane((fi ? it.mem : wm) - h.mem, w);
-            const int32_t ng = __builtin_amdgcn_readlane((fi ? it.gpu : wg) - h.gpu, w);
-            const int32_t na = __builtin_amdgcn_readlane(fi ? it.avail : wa, w);
-            const uint32_t nk = __builtin_amdgcn_readlane(fi ? it.mask : wk, w);
-            node = __builtin_amdgcn_readlane(fi ? it.orig : wo, w);
+        if (best != KEY_INF) {
+            int32_t sc, sm, sg, sa, slot;
+            uint32_t sk;
+            if (rl >= 0) {
+                sc = __builtin_amdgcn_readlane(wc, rl);
+                sm = __builtin_amdgcn_readlane(wm, rl);
+                sg = __builtin_amdgcn_readlane(wg, rl);
+                sa = __builtin_amdgcn_readlane(wa, rl);
+                sk = __builtin_amdgcn_readlane(wk, rl);
+                node = __builtin_amdgcn_readlane(wo, rl);
+                slot = __builtin_amdgcn_readlane(ws, rl);
+            } else {
+                sc = __builtin_amdgcn_readlane(it.cpu, il);
+                sm = __builtin_amdgcn_readlane(it.mem, il);
+                sg = __builtin_amdgcn_readlane(it.gpu, il);
+                sa = __builtin_amdgcn_readlane(it.avail, il);
+                sk = __builtin_amdgcn_readlane(it.mask, il);
+                node = __builtin_amdgcn_readlane(it.orig, il);
+                slot = __builtin_amdgcn_readlane(it.tag, il);
+            }
+            const bool fresh = slot < 0;  // a clean node becomes dirty row nu
+            if (fresh && nu == UCAP) {
+                stop = 2;  // dirty set full
+                break;
+            }
+            if (fresh) slot = nu++;
+            const int32_t nc = sc - __builtin_amdgcn_readfirstlane(h.cpu);
+            const int32_t nm = sm - __builtin_amdgcn_readfirstlane(h.mem);
+            const int32_t ng = sg - __builtin_amdgcn_readfirstlane(h.gpu);
+            const uint32_t pos = (uint32_t)best;
             if (lane == 0) {
-                S->rows[slot] = MwRow{nc, nm, ng, na, nk, ml, node, t};
+                S->rows[slot] = MwRow{nc, nm, ng, sa, sk, pos, node, t};
                 if (fresh) {
-                    const uint32_t rel = ml - nb;
+                    const uint32_t rel = pos - nb;
                     __hip_atomic_fetch_or(&S->bitmap[rel >> 5], 1u << (rel & 31),
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
-            // ring: the entry of job t; an older entry of the same slot dies
-            const bool me = l8 == (t & 7);
+            // ring entry t & 7 (job, slot, pos in every lane; the row in lane t & 7 only); an
+            // older entry of the same slot dies
+            const int e = t & 7;
+            const bool me = r8 == e;
             wj = me ? t : (ws == slot ? -1 : wj);
             ws = me ? slot : ws;
-            wc = me ? nc : wc;
-            wm = me ? nm : wm;
-            wg = me ? ng : wg;
-            wa = me ? na : wa;
-            wk = me ? nk : wk;
-            wp = me ? ml : wp;
-            wo = me ? node : wo;
+            wp = me ? pos : wp;
+            wc = writelane(nc, e, wc);
+            wm = writelane(nm, e, wm);
+            wg = writelane(ng, e, wg);
+            wa = writelane(sa, e, wa);
+            wk = writelane(sk, e, wk);
+            wo = writelane(node, e, wo);
+            ++placed;
         }
-        if (lane == (t & 63)) {
-            oq = h.q;
-            ov = node;
-        }
+        oq = writelane(__builtin_amdgcn_readfirstlane(h.q), t & 63, oq);
+        ov = writelane(node, t & 63, ov);
         if ((t & 63) == 63) {  // uniform: flush 64 placements
             if (oq >= 0) out[(int64_t)oq * kmax] = ov;
             oq = -1;

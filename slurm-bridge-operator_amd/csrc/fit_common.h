@@ -228,6 +228,46 @@ __device__ unsigned long long g_stamps[64][8];
 #define STAMP_FLUSH(c, n)
 #endif
 
+// Multi-node jobs (SPEC k > 1): the K smallest keys among the lane's clean candidate entries and
+// dirty-row keys, ascending, by K wave-wide extractions.  seld[i]: sel[i] is a dirty row.  kth =
+// the K-th key (INF when fewer than K exist).  Returns how many were found.
+template <int EPL>
+__device__ __forceinline__ int select_k(int K, const uint64_t (&kr)[EPL], const bool (&cl)[EPL],
+                                        const uint64_t (&dk)[UPL], uint64_t (&sel)[FIT_KMAX],
+                                        bool (&seld)[FIT_KMAX], uint64_t& kth) {
+    uint64_t ce[EPL], de[UPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) ce[k] = cl[k] ? kr[k] : KEY_INF;
+#pragma unroll
+    for (int i = 0; i < UPL; ++i) de[i] = dk[i];
+    int got = 0;
+#pragma unroll
+    for (int s = 0; s < FIT_KMAX; ++s) {
+        sel[s] = KEY_INF;
+        seld[s] = false;
+        if (s < K) {
+            uint64_t cmin = KEY_INF, dmin = KEY_INF;
+#pragma unroll
+            for (int k = 0; k < EPL; ++k) cmin = umin64(cmin, ce[k]);
+#pragma unroll
+            for (int i = 0; i < UPL; ++i) dmin = umin64(dmin, de[i]);
+            const uint64_t b = wave_min_key(umin64(cmin, dmin));
+            if (b != KEY_INF) {
+                sel[s] = b;
+                seld[s] = __ballot(dmin == b) != 0ull;
+                kth = b;
+                ++got;
+#pragma unroll
+                for (int k = 0; k < EPL; ++k) ce[k] = ce[k] == b ? KEY_INF : ce[k];
+#pragma unroll
+                for (int i = 0; i < UPL; ++i) de[i] = de[i] == b ? KEY_INF : de[i];
+            }
+        }
+    }
+    if (got < K) kth = KEY_INF;
+    return got;
+}
+
 struct CRow {  // node row of a candidate (prefetched)
     int32_t cpu, mem, gpu, avail;
     uint32_t mask;
@@ -279,14 +319,73 @@ struct CRow {  // node row of a candidate (prefetched)
             }                                                                                   \
         }                                                                                       \
         STAMP(3);                                                                               \
+        int32_t node = -1;                                                                      \
+        uint32_t newpos = 0xffffffffu;                                                          \
+        if (jkr[A] > 1) { /* multi-node job (uniform): the k smallest, all or nothing */        \
+            const int K_ = jkr[A];                                                              \
+            uint64_t sel_[FIT_KMAX];                                                            \
+            bool seld_[FIT_KMAX];                                                               \
+            uint64_t kth_ = KEY_INF;                                                            \
+            const int got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_);            \
+            if (B != KEY_INF && kth_ > B) {                                                     \
+                stop = 1;                                                                       \
+                goto done;                                                                      \
+            }                                                                                   \
+            if (got_ == K_) {                                                                   \
+                int nn_ = 0;                                                                    \
+                _Pragma("unroll") for (int i = 0; i < FIT_KMAX; ++i) nn_ += i < K_ && !seld_[i]; \
+                if (nu + nn_ > UCAP) {                                                          \
+                    stop = 2;                                                                   \
+                    goto done;                                                                  \
+                }                                                                               \
+                _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) if (s_ < K_) {         \
+                    const uint64_t b_ = sel_[s_];                                               \
+                    int32_t nd_;                                                                \
+                    if (seld_[s_]) {                                                            \
+                        int32_t o = 0;                                                          \
+                        bool hl_ = false;                                                       \
+                        _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {      \
+                            const bool hit_ = dk[i] == b_;                                      \
+                            ucpu[i] -= hit_ ? jc : 0;                                           \
+                            umem[i] -= hit_ ? jm : 0;                                           \
+                            ugpu[i] -= hit_ ? jg : 0;                                           \
+                            o = hit_ ? uorig[i] : o;                                            \
+                            hl_ |= hit_;                                                        \
+                        }                                                                       \
+                        nd_ = __builtin_amdgcn_readlane(o, __builtin_ctzll(__ballot(hl_)));     \
+                    } else {                                                                    \
+                        const uint32_t np_ = (uint32_t)b_;                                      \
+                        const NodeRec r = rec[np_];                                             \
+                        nd_ = r.orig;                                                           \
+                        if (lane == (nu & 63)) {                                                \
+                            _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i == (nu >> 6)) { \
+                                ucpu[i] = r.cpu - jc;                                           \
+                                umem[i] = r.mem - jm;                                           \
+                                ugpu[i] = r.gpu - jg;                                           \
+                                uav[i] = r.avail;                                               \
+                                umask[i] = r.mask;                                              \
+                                upos[i] = np_;                                                  \
+                                uorig[i] = nd_;                                                 \
+                            }                                                                   \
+                            const uint32_t rel = np_ - nb;                                      \
+                            bitmap[rel >> 5] |= 1u << (rel & 31);                               \
+                        }                                                                       \
+                        ++nu;                                                                   \
+                        _Pragma("unroll") for (int k = 0; k < EPL; ++k) cl[N1][k] =             \
+                            cl[N1][k] && (uint32_t)kr[N1][k] != np_;                            \
+                    }                                                                           \
+                    if (s_ == 0) node = nd_;                                                    \
+                    else if (lane == 0) out[(int64_t)jqr[A] * kmax + s_] = nd_;                 \
+                }                                                                               \
+                ++placed;                                                                       \
+            }                                                                                   \
+        } else {                                                                                \
         const uint64_t best = wave_min_key(umin64(cm, dm));                                     \
         STAMP(4);                                                                               \
         if (B != KEY_INF && best > B && __ballot(cm != KEY_INF) == 0ull) {                      \
             stop = 1; /* candidate list exhausted: rescan next round */                         \
             goto done;                                                                          \
         }                                                                                       \
-        int32_t node = -1;                                                                      \
-        uint32_t newpos = 0xffffffffu;                                                          \
         if (best != KEY_INF) {                                                                  \
             const uint64_t dmask = __ballot(dm == best);                                        \
             if (dmask) { /* a dirty row wins: update it in place */                             \
@@ -324,6 +423,7 @@ struct CRow {  // node row of a candidate (prefetched)
             }                                                                                   \
             ++placed;                                                                           \
         }                                                                                       \
+        } /* k == 1 */                                                                          \
         STAMP(5);                                                                               \
         if (lane == (t & 63)) {                                                                 \
             oq = jqr[A];                                                                        \
@@ -344,6 +444,7 @@ struct CRow {  // node row of a candidate (prefetched)
             jgr[N3] = J_.gpu;                                                                   \
             jwr[N3] = J_.wall;                                                                  \
             jpr[N3] = J_.pbit;                                                                  \
+            jkr[N3] = J_.k;                                                                     \
             jb[N3] = bnd[P.slot0 + tc_];                                                        \
         }                                                                                       \
         ++t;                                                                                    \
@@ -385,7 +486,7 @@ __device__ __forceinline__ CommitResult commit_window(
 
     uint64_t kr[4][EPL];
     bool cl[4][EPL];
-    int32_t jqr[4], jcr[4], jmr[4], jgr[4], jwr[4];
+    int32_t jqr[4], jcr[4], jmr[4], jgr[4], jwr[4], jkr[4];
     uint32_t jpr[4];
     uint64_t jb[4];
 #pragma unroll
@@ -402,6 +503,7 @@ __device__ __forceinline__ CommitResult commit_window(
         jgr[s] = J.gpu;
         jwr[s] = J.wall;
         jpr[s] = J.pbit;
+        jkr[s] = J.k;
         jb[s] = bnd[P.slot0 + tc];
     }
 #pragma unroll

@@ -12,6 +12,7 @@ constexpr int MAX_SLICES = 4;   // block-slices per job per rank (sub-slice grow
 constexpr int UCAP = 256;       // dirty-node capacity per component per round (4 per lane)
 constexpr int MAX_COMPONENT_NODES = 1 << 20;  // LDS dirty bitmap limit (128 KiB)
 constexpr uint64_t KEY_INF = ~0ull;
+constexpr int FIT_KMAX = 8;     // nodes per multi-node job (include/fitgpu.h FIT_MAX_K)
 
 // One Slurm node row in HBM, 32 B: read by fit_scan with one scalar s_load_dwordx8.
 struct alignas(32) NodeRec {

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64) void k_commit(
 // ------------------------------------------------------------------- prefilter / setup
 // out[] init, component id per job, rejected marks (FIT_REJECTED) — DESIGN.md §3.1.
 __global__ void k_prefilter(const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
-                            const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
+                            const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
                             const uint16_t* __restrict__ jk, int32_t nj, int32_t kmax,
                             const int32_t* __restrict__ ptab /* [4][32]: time,cpus,mem,comp */,
                             int32_t np, int32_t* __restrict__ out, int8_t* __restrict__ jcomp) {
@@ -64,7 +64,12 @@ __global__ void k_prefilter(const int32_t* __restrict__ jcpu, const int32_t* __r
         const int mt = ptab[p], mc = ptab[32 + p], mm = ptab[64 + p];
         rej = (mt >= 0 && jwall[q] > mt) || (mc >= 0 && jcpu[q] > mc) || (mm >= 0 && jmem[q] > mm);
     }
-    int8_t comp = rej ? (int8_t)-2 : (int8_t)ptab[96 + p];  // -1: partition has no nodes
+    // -3: invalid job (negative demand or nodes_k > kmax), -2: rejected by partition limits,
+    // -1: partition has no nodes, else component | 0x40 for a multi-node job
+    int8_t comp = rej ? (int8_t)-2 : (int8_t)ptab[96 + p];
+    if (comp >= 0 && k > 1) comp = (int8_t)(comp | 0x40);
+    if (k > kmax || jcpu[q] < 0 || jmem[q] < 0 || jwall[q] < 0 || (jgpu && jgpu[q] < 0))
+        comp = (int8_t)-3;
     jcomp[q] = comp;
     for (int i = 0; i < kmax; ++i) out[(int64_t)q * kmax + i] = (rej && i < k) ? -2 : -1;
 }
@@ -138,11 +143,11 @@ extern "C" int fit_debug_commit_stamps(unsigned long long* out /* 64 x 8 */) {
 #endif
 
 hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* jmem,
-                            const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
+                            const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
                             int32_t nj, int32_t kmax, const int32_t* ptab, int32_t np,
                             int32_t* out, int8_t* jcomp) {
     if (nj == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prefilter, dim3((nj + 255) / 256), dim3(256), 0, st, jcpu, jmem, jwall,
+    hipLaunchKernelGGL(k_prefilter, dim3((nj + 255) / 256), dim3(256), 0, st, jcpu, jmem, jgpu, jwall,
                        jpart, jk, nj, kmax, ptab, np, out, jcomp);
     return hipGetLastError();
 }

@@ -53,6 +53,16 @@ __device__ __forceinline__ void release_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
 }
 
+// Windows holding a multi-node job: the single-wave commit (fit_common.h), kept out of line so
+// its registers are allocated apart from the decider / helper / worker loops.
+__device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan& P, NodeRec* rec,
+                                                          const uint64_t* cand,
+                                                          const uint64_t* bnd, const JobRec* wjob,
+                                                          int32_t* out, int kmax,
+                                                          uint32_t* bitmap) {
+    return commit_window<1>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
+}
+
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
     const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
@@ -61,7 +71,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk,
     uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob,
-    int32_t* __restrict__ out, int kmax, int64_t* __restrict__ wbusy) {
+    int32_t* __restrict__ out, int kmax, int64_t* __restrict__ wbusy,
+    const int32_t* __restrict__ jpk) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
 
@@ -128,7 +139,27 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             __syncthreads();
             if (s_fail) break;  // block-uniform
             const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            const CommitResult R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax);
+            // a window holding a multi-node job is committed by wave 0 alone (commit_window
+            // handles k > 1); the decider/helper pipeline covers k = 1 windows
+            CommitResult R;
+            if (jpk[cursor + w] == jpk[cursor]) {
+                R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax);
+            } else {
+                if (wave == 0) {
+                    const CommitResult r0 =
+                        engine_commit_single(c, P, rec, cand, bnd, wjob, out, kmax, M->bitmap);
+                    if (lane == 0) {
+                        M->res[0] = r0.done;
+                        M->res[1] = r0.stop;
+                        M->res[2] = r0.dirty;
+                        M->res[3] = r0.placed;
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row write-back stores
+                }
+                __syncthreads();
+                R = CommitResult{M->res[0], M->res[1], M->res[2], M->res[3]};
+                __syncthreads();
+            }
             if (R.stop == 3) {  // commit watchdog
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
                 break;
@@ -230,12 +261,12 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
                          const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
-                         int32_t* out, int kmax, int64_t* wbusy) {
+                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk) {
     hipLaunchKernelGGL(k_engine, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,
                        static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),
                        static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,
                        rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, out, kmax,
-                       wbusy);
+                       wbusy, jpk);
     return hipGetLastError();
 }
 

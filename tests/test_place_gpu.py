@@ -11,18 +11,18 @@ from oracle import pyoracle as po
 pytestmark = pytest.mark.gpu
 
 
-def run_engine(nodes, jobs, parts, **kw):
+def run_engine(nodes, jobs, parts, kmax=1, **kw):
     with Engine(**kw) as e:
         e.load_nodes(nodes)
         e.load_partitions(parts)
-        out, st = e.place(jobs)
+        out, st = e.place(jobs, kmax=kmax)
         fin = e.read_nodes()
     return out, st, fin
 
 
-def check_parity(nodes, jobs, parts, **kw):
-    ref, rst, rfin = po.ref_place(nodes, jobs, parts)
-    out, st, fin = run_engine(nodes, jobs, parts, **kw)
+def check_parity(nodes, jobs, parts, kmax=1, **kw):
+    ref, rst, rfin = po.ref_place(nodes, jobs, parts, kmax=kmax)
+    out, st, fin = run_engine(nodes, jobs, parts, kmax=kmax, **kw)
     assert np.array_equal(out, ref), f"first mismatch at job {int(np.argmax(out[:, 0] != ref[:, 0]))}"
     for a, b in zip(fin, rfin):
         assert np.array_equal(a, b)
@@ -52,3 +52,50 @@ def test_c3_prefix():
 def test_window_policies_c2(wmin, wmax):
     nodes, jobs, parts = synth.make_config("c2", 512, 8192)
     check_parity(nodes, jobs, parts, window_min=wmin, window_max=wmax)
+
+
+# ---- multi-node jobs (SPEC k > 1, config C4: GPU-heavy nodes, nodes_k in {1, 2, 4, 8}) ----------
+@pytest.mark.parametrize("engine", ["persistent", "rounds"])
+@pytest.mark.parametrize("nn,jj", [(64, 1024), (512, 8192), (4096, 65536)])
+def test_c4_multi_node(nn, jj, engine, monkeypatch):
+    if engine == "rounds":
+        monkeypatch.setenv("FIT_ENGINE", "rounds")
+    nodes, jobs, parts = synth.make_config("c4", nn, jj)
+    assert jobs.nodes_k.max() > 1
+    st = check_parity(nodes, jobs, parts, kmax=8)
+    assert st["placed"] > 0
+
+
+def test_c4_prefix():
+    nodes, jobs, parts = synth.make_config("c4", 20000, 100000)
+    check_parity(nodes, jobs, parts, kmax=8)
+
+
+def test_c4_window_policies():
+    nodes, jobs, parts = synth.make_config("c4", 512, 8192)
+    for wmin, wmax in [(1, 1), (1, 8), (64, 64)]:
+        check_parity(nodes, jobs, parts, kmax=8, window_min=wmin, window_max=wmax)
+
+
+def test_multi_node_edge_cases():
+    # 8 identical 64-cpu nodes; jobs needing k nodes of 20 cpus: three k=8 jobs fill the cluster,
+    # k=1 jobs keep flowing; all-or-nothing (no partial allocation)
+    nodes, _, parts = synth.make_c1()
+    k = np.array([8, 8, 1, 2, 1, 4, 8, 1] * 8, np.uint16)
+    n = len(k)
+    jobs = synth.Jobs(np.full(n, 20, np.int32), np.full(n, 1000, np.int32), np.zeros(n, np.int32),
+                      np.full(n, 60, np.int32), np.zeros(n, np.uint16), k)
+    st = check_parity(nodes, jobs, parts, kmax=8)
+    assert st["unplaced"] > 0
+    # kmax larger than any k: unused columns stay -1
+    check_parity(nodes, jobs, parts, kmax=8)
+
+
+def test_nodes_k_above_kmax_is_rejected():
+    nodes, jobs, parts = synth.make_config("c4", 64, 256)
+    from fitgpu import FitError
+    with Engine() as e:
+        e.load_nodes(nodes)
+        e.load_partitions(parts)
+        with pytest.raises(FitError):
+            e.place(jobs, kmax=2)
