@@ -82,7 +82,8 @@ def parse_args():
     ap.add_argument("--workload", default="c3", choices=["c2", "c3"])
     ap.add_argument("--cpu-sample", type=int, default=40000, help="jobs in the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pmc-json", default=None, help="profiles/*_pmc.json with measured HBM bytes/launch")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="PMC summary (tools/gpu_pmc.sh + tools/pmc_json.py) with HBM bytes/launch")
     ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
                     help="N>1 split: auto = partition components when there are >= N of them")
     return ap.parse_args()

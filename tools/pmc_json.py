@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""rocprofv3 --pmc passes (tools/gpu_pmc.sh, --output-format csv) → per-kernel counters per launch.
+
+    python tools/pmc_json.py gpurun_out/<tag>_pmc > profiles/<tag>_pmc.json
+
+HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE are in KiB and come
+from separate passes; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+doubled (the correction the guide prescribes; other access widths are uncalibrated there).
+Infinity-Cache (MALL) hits are counted by these counters, not excluded.
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0].split("::")[-1]
+
+
+def main(prefix):
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
+    for path in sorted(glob.glob(prefix + "*/pmc_counter_collection.csv")):
+        acc = defaultdict(float)
+        for r in csv.DictReader(open(path)):
+            acc[(short(r["Kernel_Name"]), r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (k, _, c), v in acc.items():
+            per[k][c].append(v)
+    out = {"source": prefix, "note": __doc__.strip().splitlines()[2].strip()}
+    for k, cs in per.items():
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = {"launches_profiled": max(len(v) for v in cs.values())}
+        d.update({c: round(v, 1) for c, v in m.items()})
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            d["hbm_read_bytes_per_launch"] = round(m["FETCH_SIZE"] * 1024 * 2)
+            d["hbm_write_bytes_per_launch"] = round(m["WRITE_SIZE"] * 1024)
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes_per_launch"] + d["hbm_write_bytes_per_launch"]
+        if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
+            d["l2_hit_rate"] = round(m["TCC_HIT_sum"] / max(m["TCC_HIT_sum"] + m["TCC_MISS_sum"], 1), 4)
+        out[k] = d
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
