@@ -36,7 +36,7 @@ def commit_bytes_per_job(entries: int) -> int:
     return entries * 8 + 32 + 8 + 4  # candidate keys + job row + bound + placement
 
 
-def kernel_table(agg, stats, steps, world, evals_local):
+def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_commit")):
     """Per-kernel live timings (engine HIP events) and their rooflines.
 
     Persistent engine (engine == 1): ONE k_engine launch per step; its duration is ms_device.  The
@@ -64,11 +64,11 @@ def kernel_table(agg, stats, steps, world, evals_local):
     entries = 64 * (world if stats[-1]["shard_mode"] == 1 else 1)
     commit_gbs = jobs_resolved / rounds * commit_bytes_per_job(entries) / (commit_ms * 1e-3) / 1e9
     return {
-        "k_scan": {"ms_per_launch": round(scan_ms, 4), "launches": rounds, "bound": "valu",
+        names[0]: {"ms_per_launch": round(scan_ms, 4), "launches": rounds, "bound": "valu",
                    "achieved": round(scan_tops, 3), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
                    "frac": round(scan_tops / PEAK_VALU_TOPS, 4),
                    "hbm_gbs_algorithmic": round(evals_per_launch * SCAN_BYTES_PER_EVAL / (scan_ms * 1e-3) / 1e9, 1)},
-        "k_commit": {"ms_per_launch": round(commit_ms, 4), "launches": rounds, "bound": "latency",
+        names[1]: {"ms_per_launch": round(commit_ms, 4), "launches": rounds, "bound": "latency",
                      "achieved": round(commit_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(commit_gbs / PEAK_HBM_GBS, 5)},
     }
@@ -79,8 +79,10 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3"])
-    ap.add_argument("--cpu-sample", type=int, default=40000, help="jobs in the CPU baseline sample")
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
+                    help="c3: BASELINE headline (100k x 1M); c5: the same with a 1,024-slot backfill horizon")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="jobs in the CPU baseline sample (default 40,000; c5: 3,000)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/gpu_pmc.sh + tools/pmc_json.py) with HBM bytes/launch")
@@ -113,7 +115,11 @@ def main():
         nid = None
 
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
-    nodes, jobs, parts = synth.make_config(a.workload)
+    tl = a.workload == "c5"
+    if tl:
+        nodes, tline, jobs, parts = synth.make_c5()
+    else:
+        nodes, jobs, parts = synth.make_config(a.workload)
     dev = torch.device("cuda", local)
     T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
     d_nodes = [T(nodes.cpu_free), T(nodes.mem_free), T(nodes.gpu_free), T(nodes.avail_min),
@@ -121,6 +127,9 @@ def main():
     d_jobs = [T(jobs.cpu), T(jobs.mem), T(jobs.gpu), T(jobs.wall), T(jobs.part.view(np.int16)),
               T(jobs.nodes_k.view(np.int16))]
     d_out = torch.empty(jobs.j, dtype=torch.int32, device=dev)
+    if tl:
+        d_rel = [T(x) for x in (tline.off, tline.slot, tline.cpu, tline.mem, tline.gpu)]
+        d_start = torch.empty(jobs.j, dtype=torch.int32, device=dev)
 
     mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
     eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
@@ -128,6 +137,9 @@ def main():
 
     def step():
         eng.load_nodes_device(*d_nodes)
+        if tl:
+            eng.load_timeline_device(tline.slots, tline.slot_min, *d_rel)
+            return eng.place_tl_device(*d_jobs[:5], d_out, d_start)
         return eng.place_device(*d_jobs, d_out, kmax=1)
 
     for _ in range(a.warmup):
@@ -162,7 +174,8 @@ def main():
         agg["evals"] = int(t.item())
     used_mode = {0: "1 GPU", 1: f"node-sharded x{world} (RCCL allgather + u64 min-allreduce per round)",
                  2: f"partition-component-sharded x{world} (one RCCL merge)"}[stats[-1]["shard_mode"]]
-    kernels = kernel_table(agg, stats, a.steps, world, evals_local)
+    kernels = kernel_table(agg, stats, a.steps, world, evals_local,
+                           ("k_scan_tl", "k_commit_tl") if tl else ("k_scan", "k_commit"))
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_launch"] * kernels[k]["launches"])
     k = kernels[dominant]
     traffic = None
@@ -174,16 +187,21 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import pyoracle as po
-        sample = min(a.cpu_sample, jobs.j)
+        sample = min(a.cpu_sample or (3000 if tl else 40000), jobs.j)
         sub = synth.Jobs(*(x[:sample] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part,
                                                   jobs.nodes_k)))
         t = time.perf_counter()
-        _, cst, _ = po.ref_place(nodes, sub, parts)
+        if tl:
+            _, _, cst, _ = po.ref_place_tl(nodes, tline, sub, parts)
+            what = "oracle/fitref_tl.c ref_place_tl (C restatement of SPEC §2b, dense timelines)"
+        else:
+            _, cst, _ = po.ref_place(nodes, sub, parts)
+            what = "oracle/fitref.c ref_place (C restatement of the scalar sequential path)"
         ct = time.perf_counter() - t
         cpu = {"value": round(sample / ct, 2), "unit": "placements/s", "cores": 1, "kind": "port",
                "evals_per_s": round(cst["evals"] / ct, 1),
-               "sample": f"first {sample} jobs of {a.workload} vs all {nodes.n} nodes, oracle/fitref.c "
-                         f"ref_place (C restatement of the scalar sequential path), 1 thread, {ct:.1f}s",
+               "sample": f"first {sample} jobs of {a.workload} vs all {nodes.n} nodes, {what}, 1 thread, "
+                         f"{ct:.1f}s",
                "host_cpu": _cpu_model()}
 
     line = {
@@ -192,9 +210,11 @@ def main():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic (splitmix64 generator, fitgpu/synth.py; DESIGN.md §5)",
         "config": {"workload": a.workload, "nodes": nodes.n, "jobs": jobs.j, "partitions": parts.p,
+                   **({"slots": tline.slots, "slot_min": tline.slot_min} if tl else {}),
                    "parallelism": used_mode, "components": stats[-1]["components"]},
         "fit_evals_per_s": {"useful": round(agg["useful_evals"] / el, 1), "performed": round(agg["evals"] / el, 1)},
         "rounds_per_step": agg["rounds"] / a.steps,
+        "round_stops_per_step": {"rescan": stats[-1]["stops_rescan"], "dirty_full": stats[-1]["stops_dirty"]},
         "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
     }
     if cpu:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 2
+#define FITGPU_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -142,6 +142,39 @@ int fit_read_nodes(fit_ctx* ctx, int32_t* cpu_free, int32_t* mem_free, int32_t* 
  * replacement for the allocation-blind sum of GetPartitionCapacity (node.go:183-190). */
 int fit_partition_free(fit_ctx* ctx, int32_t p, int64_t* cpu, int64_t* mem_mib, int64_t* gpu);
 
+/* ---- time-windowed backfill (BASELINE config C5) -------------------------
+ * Each node's free resources over a horizon of `slots` slots of `slot_min` minutes (slots <=
+ * 1024): the node table of the last fit_load_nodes is the state at slot 0, and the jobs already
+ * running hand resources back at their end — release events, CSR by node id: node x's events are
+ * [rel_off[x], rel_off[x+1]) with non-decreasing rel_slot (slot <= 0 = already free) and amounts
+ * >= 0.  A node is usable for slots t < avail_min / slot_min.  Call after fit_load_nodes (which
+ * drops the timeline); rel_off NULL = no releases.  Host pointers; rel_off has n+1 entries.
+ * The walltime source is the job's --time (pkg/slurm-bridge-operator/parse.go:84-91) and the
+ * squeue EndTime of running jobs; the partition MaxTime check is parseResources' (parse.go:128-138). */
+int fit_load_timeline(fit_ctx* ctx, int32_t slots, int32_t slot_min, const int32_t* rel_off,
+                      const int32_t* rel_slot, const int32_t* rel_cpu, const int32_t* rel_mem,
+                      const int32_t* rel_gpu);
+/* Same with device pointers; n_rel = rel_off[n] (the caller knows it; not read back). */
+int fit_load_timeline_device(fit_ctx* ctx, int32_t slots, int32_t slot_min,
+                             const int32_t* rel_off, int64_t n_rel, const int32_t* rel_slot,
+                             const int32_t* rel_cpu, const int32_t* rel_mem,
+                             const int32_t* rel_gpu);
+/* Sequential priority-order backfill: each job (one node, nodes_k = 1) gets the node and the
+ * earliest start slot at which its demand fits for ceil(wall / slot_min) consecutive slots, best
+ * fit among the nodes with that start; the reservation is committed and later
+ * jobs see it.  out_node[j]: node id, FIT_UNPLACED (no start inside the horizon) or FIT_REJECTED;
+ * out_start[j]: start slot, -1 when not placed.  Host pointers. */
+int fit_place_tl(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem,
+                 const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out_node,
+                 int32_t* out_start, fit_stats* stats);
+/* Same with device pointers (inputs resident in HBM, outputs written in HBM). */
+int fit_place_tl_device(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem,
+                        const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                        int32_t* out_node, int32_t* out_start, fit_stats* stats);
+/* Current timelines, dense [n][slots] per column, host pointers (n * slots entries each).  Slots
+ * where a node is unusable, and nodes outside every partition, read -1. */
+int fit_read_timeline(fit_ctx* ctx, int32_t* cpu, int32_t* mem, int32_t* gpu);
+
 /* ---- ingest / demand helpers (host code, mirrors of the reference Go functions) -------- */
 /* ParseDuration (pkg/slurm-agent/parse.go:36-109): 0 ok, FIT_E_UNLIMITED, FIT_E_PARSE. */
 int fit_parse_duration(const char* s, int64_t* out_ns);
@@ -184,6 +217,23 @@ int fit_job_demand(const fit_job_resources* r, int32_t* cpu, int32_t* mem_mib, i
 /* GetPartitionCapacity (pkg/slurm-virtual-kubelet/node.go:169-199), reference arithmetic. */
 void fit_partition_capacity(const fit_node* nodes, int32_t n, int64_t* cpu, int64_t* memory,
                             int64_t* gpu, int64_t* pods);
+
+/* ---- node-table ingest -------------------------------------------------
+ * `scontrol show nodes` text → the engine's node columns (fit_load_nodes order and meaning).
+ * Records are split and CPUTot/CPUAlloc/RealMemory/AllocMem parsed exactly as Client.Nodes +
+ * parseNode (slurm.go:354-363, parse.go:291-308); added: Gres/GresUsed gpu counts (gpu_free =
+ * Gres − GresUsed; the reference never sets Gpus/AlloGpus), Partitions= → part_mask bit p for
+ * the p-th name of `partitions` (np NUL-separated names), State (DOWN, DRAIN, FAIL, MAINT, '*'
+ * not responding, ...) → part_mask 0 (never placed), NodeName → `names` (NUL-separated, may be
+ * NULL).  avail_min = INT32_MAX.  Returns the record count, FIT_E_INVAL (cap / buffer too small),
+ * FIT_E_PARSE (malformed gres count). */
+int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32_t cap,
+                     int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free, int32_t* avail_min,
+                     uint32_t* part_mask, char* names, int32_t names_len);
+/* Slurm hostlist expansion ("node[01-03,7],gpu[1-2]-ib" → node01 node02 node03 node07 gpu1-ib
+ * gpu2-ib), NUL-separated into buf; returns the count, FIT_E_PARSE or FIT_E_INVAL (buf too
+ * small).  The fix for parsePartition's split of "Nodes=node[1-3,5]" (parse.go:278-289). */
+int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen);
 
 #ifdef __cplusplus
 }

@@ -78,6 +78,21 @@ uint64_t ref_key(int32_t node_id, int32_t cpu_free, int32_t mem_free, int32_t gp
                  int32_t avail, uint32_t mask, int32_t cpu, int32_t mem, int32_t gpu, int32_t wall,
                  int32_t part);
 
+/* ---- SPEC §2b time-windowed backfill (oracle/fitref_tl.c) — parity unpinned vs the reference,
+ * which has no reservation timeline.  tl: dense [n][H][3] (cpu, mem, gpu). */
+int ref_build_timeline(int32_t n, int32_t H, int32_t slot_min, const int32_t* cpu_free,
+                       const int32_t* mem_free, const int32_t* gpu_free, const int32_t* avail_min,
+                       const int32_t* rel_off, const int32_t* rel_slot, const int32_t* rel_cpu,
+                       const int32_t* rel_mem, const int32_t* rel_gpu, int32_t* tl);
+int32_t ref_slots(int32_t wall, int32_t slot_min);
+uint64_t ref_key_tl(int32_t x, int32_t H, const int32_t* row, uint32_t mask, int32_t cpu,
+                    int32_t mem, int32_t gpu, int32_t d, int32_t part, int32_t* out_start);
+int ref_place_tl(int32_t n, int32_t H, int32_t slot_min, int32_t* tl, const uint32_t* part_mask,
+                 int32_t p, const int32_t* max_time, const int32_t* max_cpus,
+                 const int32_t* max_mem, int32_t j, const int32_t* cpu, const int32_t* mem,
+                 const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out_node,
+                 int32_t* out_start, int64_t* stats);
+
 /* splitmix64 twin of fitgpu/synth.py (rnd / uni). */
 uint64_t ref_rnd(uint64_t seed, uint32_t stream, uint64_t idx);
 

@@ -19,7 +19,7 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "liboracle.so")
-        srcs = [os.path.join(_HERE, f) for f in ("fitref.c", "round_model.c", "fitref.h")]
+        srcs = [os.path.join(_HERE, f) for f in ("fitref.c", "fitref_tl.c", "round_model.c", "fitref.h", "Makefile")]
         if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
             subprocess.check_call(["make", "-s", "-C", _HERE])
         _LIB = C.CDLL(path)
@@ -27,6 +27,7 @@ def lib():
         _LIB.ref_rnd.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64]
         _LIB.ref_key.restype = C.c_uint64
         _LIB.ref_parse_array_len.restype = C.c_int64
+        _LIB.ref_key_tl.restype = C.c_uint64
     return _LIB
 
 
@@ -89,3 +90,40 @@ def model_place(nodes, jobs, parts, slice=2048, ks=8, km=32, ucap=256, wmin=256,
     keys = ["rounds", "scan_evals", "dirty_evals", "stops_rescan", "stops_ucap", "commits",
             "max_window", "placed"]
     return out, {k: int(v) for k, v in zip(keys, st)}, (cf, mf, gf)
+
+
+# ---- SPEC §2b time-windowed backfill (oracle/fitref_tl.c) ----------------------------------------
+def ref_build_timeline(nodes, tline):
+    """Dense [n, H, 3] int32 timeline (cpu, mem, gpu) of DESIGN.md §2b."""
+    n, H = nodes.n, tline.slots
+    tl = np.empty((n, H, 3), np.int32)
+    I32 = C.c_int32
+    cols = [np.ascontiguousarray(a, np.int32) for a in (nodes.cpu_free, nodes.mem_free, nodes.gpu_free,
+                                                        nodes.avail_min)]
+    rel = [np.ascontiguousarray(a, np.int32) for a in (tline.off, tline.slot, tline.cpu, tline.mem, tline.gpu)]
+    rc = lib().ref_build_timeline(I32(n), I32(H), I32(tline.slot_min), *(_p(a, I32) for a in cols),
+                                  *(_p(a, I32) for a in rel), _p(tl, I32))
+    if rc != 0:
+        raise ValueError("ref_build_timeline: invalid input")
+    return tl
+
+
+def ref_place_tl(nodes, tline, jobs, parts, tl=None):
+    """SPEC §2b sequential backfill.  Returns (node[J], start[J], stats dict, final dense timeline)."""
+    tl = ref_build_timeline(nodes, tline) if tl is None else np.ascontiguousarray(tl, np.int32).copy()
+    I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
+    mk = np.ascontiguousarray(nodes.part_mask, np.uint32)
+    pt = [np.ascontiguousarray(a, np.int32) for a in (parts.max_time_min, parts.max_cpus_per_node,
+                                                      parts.max_mem_per_node)]
+    jb = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
+    jp = np.ascontiguousarray(jobs.part, np.uint16)
+    node = np.empty(jobs.j, np.int32)
+    start = np.empty(jobs.j, np.int32)
+    st = np.zeros(4, np.int64)
+    rc = lib().ref_place_tl(I32(nodes.n), I32(tline.slots), I32(tline.slot_min), _p(tl, I32), _p(mk, U32),
+                            I32(parts.p), *(_p(a, I32) for a in pt), I32(jobs.j), *(_p(a, I32) for a in jb),
+                            _p(jp, U16), _p(node, I32), _p(start, I32), _p(st, C.c_int64))
+    if rc != 0:
+        raise ValueError("ref_place_tl: invalid input")
+    stats = dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3]))
+    return node, start, stats, tl

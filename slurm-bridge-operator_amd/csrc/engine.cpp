@@ -49,6 +49,26 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
                          const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
                          int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk);
+// time-windowed backfill (fit_timeline.hip)
+hipError_t launch_build_tl(hipStream_t st, const int32_t* cpu, const int32_t* mem,
+                           const int32_t* gpu, const int32_t* av, const int32_t* perm,
+                           int32_t nn, int32_t H, int32_t slot_min, const int32_t* off,
+                           const int32_t* rs, const int32_t* rc, const int32_t* rm,
+                           const int32_t* rg, Seg* slab, int32_t* segcnt, uint32_t* err);
+hipError_t launch_scan_tl(int blocks, hipStream_t st, const NodeRec* rec, const Seg* slab,
+                          const int32_t* segcnt, const int32_t* jl, const int32_t* jcpu,
+                          const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
+                          const uint16_t* jpart, const CompPlan* plan, int ncomp, uint64_t* cand,
+                          uint64_t* bnd, JobRec* wjob, int32_t H, int32_t slot_min);
+size_t commit_tl_lds_bytes(int32_t max_component_nodes);
+hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, const NodeRec* rec,
+                            Seg* slab, int32_t* segcnt, const CompPlan* plan,
+                            const uint64_t* cand, int64_t rank_stride, int nranks,
+                            const uint64_t* bnd, const JobRec* wjob, int32_t* out, int32_t* outs,
+                            CommitResult* res, int32_t H);
+hipError_t launch_expand_tl(hipStream_t st, const NodeRec* rec, const Seg* slab,
+                            const int32_t* segcnt, int32_t nn, int32_t H, int32_t* oc,
+                            int32_t* om, int32_t* og);
 }  // namespace fitgpu
 
 using namespace fitgpu;
@@ -197,11 +217,25 @@ struct fit_ctx {
     HBuf<int8_t> h_jcomp;
     std::vector<int32_t> h_jl, h_jpk;
 
+    // time-windowed backfill: per-node run lists, built from the node
+    // table + release events by fit_load_timeline
+    int32_t tl_slots = 0, tl_slot_min = 0;
+    bool have_tl = false;
+    DBuf<Seg> slab;
+    DBuf<int32_t> segcnt, outs, rel_off, rel_slot, rel_cpu, rel_mem, rel_gpu;
+    DBuf<uint32_t> tl_err;
+    HBuf<uint32_t> h_tl_err;
+
     ~fit_ctx() {
         for (auto* b : {&col_cpu, &col_mem, &col_gpu, &col_av, &perm, &jcpu, &jmem, &jgpu,
                         &jwall, &out, &jl, &jpk})
             b->release();
         rec.release();
+        for (auto* b : {&segcnt, &outs, &rel_off, &rel_slot, &rel_cpu, &rel_mem, &rel_gpu})
+            b->release();
+        slab.release();
+        tl_err.release();
+        h_tl_err.release();
         col_mask.release();
         d_ptab.release();
         jpart.release();
@@ -294,6 +328,7 @@ int load_nodes_common(fit_ctx* c, int32_t n) {
     HIP_TRY(hipStreamSynchronize(c->st));
     c->n = n;
     c->have_nodes = true;
+    c->have_tl = false;  // a timeline belongs to the node table it was built from
     return 0;
 }
 
@@ -429,24 +464,12 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     return 0;
 }
 
-// ------------------------------------------------------------------------ placement
-int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
-               const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
-               int32_t* out, fit_stats* stats) {
-    const double t0 = now_ms();
-    fit_stats S;
-    memset(&S, 0, sizeof S);
-    S.jobs = J;
-    hipStream_t st = c->st;
-    // 1. prefilter: out[] init, FIT_REJECTED, component per job
-    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
-    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
-                             c->jcomp.p));
-    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    // 2. per-component job lists in priority order (stable)
+// Per-component job lists in priority order (stable) from the prefilter's component ids
+// (h_jcomp, on the host); uploads jl / jpk.  jb[k] .. jb[k+1] = component k's list range.
+int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& jb) {
     const int C = c->ncomp;
-    std::vector<int32_t> jb(C + 1, 0);
+    jb.assign(C + 1, 0);
+    hipStream_t st = c->st;
     for (int32_t q = 0; q < J; ++q) {
         int8_t k = c->h_jcomp.p[q];
         if (k >= 0) jb[(k & 0x3f) + 1]++;
@@ -476,6 +499,29 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     HIP_TRY(hipMemcpyAsync(c->jpk.p, c->h_jpk.data(), sizeof(int32_t) * (JA + 1),
                            hipMemcpyHostToDevice, st));
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
+    return 0;
+}
+
+// ------------------------------------------------------------------------ placement
+int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+               const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
+               int32_t* out, fit_stats* stats) {
+    const double t0 = now_ms();
+    fit_stats S;
+    memset(&S, 0, sizeof S);
+    S.jobs = J;
+    hipStream_t st = c->st;
+    // 1. prefilter: out[] init, FIT_REJECTED, component per job
+    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
+                             c->jcomp.p));
+    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // 2. per-component job lists in priority order (stable)
+    const int C = c->ncomp;
+    std::vector<int32_t> jb;
+    int rc0 = build_job_lists(c, J, S, jb);
+    if (rc0) return rc0;
 
     // world > 1: split by components (each rank owns whole components, no per-round exchange)
     // or by nodes (north_star: every rank scans 1/world of every component, RCCL each round)
@@ -619,6 +665,157 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     S.unplaced = J - S.placed - S.rejected;
     S.ms_total = now_ms() - t0;
     if (stats) *stats = S;
+    return 0;
+}
+
+// ----------------------------------------------------------- time-windowed backfill
+// SPEC §2b: the same speculative rounds as the plain fit (host-driven loop), with run-list
+// scans / commits (fit_timeline.hip).  world > 1 always splits by nodes: every rank scans its
+// share of each component, the candidate sections are exchanged each round and the identical
+// deterministic commit runs on every rank over replicated run lists.
+int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
+                  const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out,
+                  int32_t* outs, fit_stats* stats) {
+    const double t0 = now_ms();
+    fit_stats S;
+    memset(&S, 0, sizeof S);
+    S.jobs = J;
+    hipStream_t st = c->st;
+    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nullptr, J, 1, c->d_ptab.p, c->np, out,
+                             c->jcomp.p));
+    if (J > 0) HIP_TRY(hipMemsetAsync(outs, 0xff, sizeof(int32_t) * J, st));
+    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int C = c->ncomp;
+    std::vector<int32_t> jb;
+    int rc = build_job_lists(c, J, S, jb);
+    if (rc) return rc;
+    const bool node_sharded = c->world > 1;
+    const int shards = c->world, srank = c->rank;
+    S.shard_mode = node_sharded ? FIT_SHARD_NODES : 0;
+    S.components = C;
+    std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
+    if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||
+        c->h_res.ensure(C + 1))
+        return FIT_E_OOM;
+    int32_t maxlen = 1;
+    for (int k = 0; k < C; ++k) maxlen = std::max(maxlen, c->nb[k + 1] - c->nb[k]);
+    const size_t lds = commit_tl_lds_bytes(maxlen);
+    float ms;
+    for (;;) {
+        int64_t blocks = 0, slots = 0, cand_n = 0, evals = 0;
+        int epl = 1;
+        bool any = false;
+        for (int k = 0; k < C; ++k) {
+            CompPlan& P = c->h_plan.p[k];
+            memset(&P, 0, sizeof P);
+            P.nb = c->nb[k];
+            P.ne = c->nb[k + 1];
+            const int32_t len = P.ne - P.nb;
+            const int32_t per = (len + shards - 1) / shards;
+            P.sb = std::min(P.ne, P.nb + per * srank);
+            P.se = std::min(P.ne, P.sb + per);
+            P.sub = std::max(MIN_SUB, (per + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
+            P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
+            epl = std::max(epl, (shards * P.nslice * KS + 63) / 64);
+            P.jbase = cur[k];
+            P.w = std::min(win[k], jb[k + 1] - cur[k]);
+            P.blk0 = (int32_t)blocks;
+            P.cand_off = cand_n;
+            P.slot0 = (int32_t)slots;
+            if (P.w > 0) {
+                any = true;
+                blocks += (int64_t)((P.w + SCAN_JOBS - 1) / SCAN_JOBS) * P.nslice;
+                cand_n += (int64_t)P.w * P.nslice * KS;
+                slots += P.w;
+                evals += (int64_t)P.w * (P.se - P.sb);
+            }
+        }
+        if (!any) break;
+        S.rounds++;
+        S.evals += evals;
+        if (c->cand.ensure((size_t)cand_n * shards) || c->bnd.ensure(slots) ||
+            c->wjob.ensure(slots))
+            return FIT_E_OOM;
+        HIP_TRY(hipMemcpyAsync(c->plan.p, c->h_plan.p, sizeof(CompPlan) * C, hipMemcpyHostToDevice,
+                               st));
+        HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * slots, st));
+        HIP_TRY(hipEventRecord(c->ev[0], st));
+        HIP_TRY(launch_scan_tl((int)blocks, st, c->rec.p, c->slab.p, c->segcnt.p, c->jl.p, cpu, mem,
+                               gpu, wall, part, c->plan.p, C, c->cand.p + (size_t)srank * cand_n,
+                               c->bnd.p, c->wjob.p, c->tl_slots, c->tl_slot_min));
+        HIP_TRY(hipEventRecord(c->ev[1], st));
+        if (node_sharded) {
+            rc = xchg(c, FIT_XCHG_ALLGATHER_U64, c->cand.p, cand_n);
+            if (!rc) rc = xchg(c, FIT_XCHG_MIN_U64, c->bnd.p, slots);
+            if (rc) return rc;
+        }
+        HIP_TRY(hipEventRecord(c->ev[2], st));
+        HIP_TRY(launch_commit_tl(C, epl, lds, st, c->rec.p, c->slab.p, c->segcnt.p, c->plan.p,
+                                 c->cand.p, cand_n, shards, c->bnd.p, c->wjob.p, out, outs,
+                                 c->res.p, c->tl_slots));
+        HIP_TRY(hipEventRecord(c->ev[3], st));
+        HIP_TRY(hipMemcpyAsync(c->h_res.p, c->res.p, sizeof(CommitResult) * C,
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        S.ms_scan += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        S.ms_exchange += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        S.ms_commit += ms;
+        for (int k = 0; k < C; ++k) {
+            const CompPlan& P = c->h_plan.p[k];
+            if (P.w == 0) continue;
+            const CommitResult& R = c->h_res.p[k];
+            if (R.done < 0 || R.done > P.w)
+                return fail(FIT_E_HIP, "commit returned %d of window %d", R.done, P.w);
+            cur[k] += R.done;
+            S.placed += R.placed;
+            if (R.stop == 1) S.stops_rescan++;
+            if (R.stop == 2) S.stops_dirty++;
+            const int32_t nw = R.stop ? 2 * R.done : 2 * P.w;
+            win[k] = std::max(c->wmin, std::min(c->wmax, nw));
+        }
+    }
+    S.ms_device = S.ms_scan + S.ms_exchange + S.ms_commit;
+    S.unplaced = J - S.placed - S.rejected;
+    S.ms_total = now_ms() - t0;
+    if (stats) *stats = S;
+    return 0;
+}
+
+int load_timeline_impl(fit_ctx* c, int32_t slots, int32_t slot_min, int64_t ne) {
+    if (c->segcnt.ensure(std::max(c->nn, 1)) ||
+        c->slab.ensure((size_t)std::max(c->nn, 1) * TL_MAX_SLOTS) || c->tl_err.ensure(1) ||
+        c->h_tl_err.ensure(1))
+        return FIT_E_OOM;
+    HIP_TRY(hipMemsetAsync(c->tl_err.p, 0, 4, c->st));
+    HIP_TRY(launch_build_tl(c->st, c->col_cpu.p, c->col_mem.p, c->col_gpu.p, c->col_av.p,
+                            c->perm.p, c->nn, slots, slot_min, ne >= 0 ? c->rel_off.p : nullptr,
+                            c->rel_slot.p, c->rel_cpu.p, c->rel_mem.p, c->rel_gpu.p, c->slab.p,
+                            c->segcnt.p, c->tl_err.p));
+    HIP_TRY(hipMemcpyAsync(c->h_tl_err.p, c->tl_err.p, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (c->h_tl_err.p[0])
+        return fail(FIT_E_INVAL, "release events: slots must be non-decreasing per node and "
+                                 "amounts >= 0");
+    c->tl_slots = slots;
+    c->tl_slot_min = slot_min;
+    c->have_tl = true;
+    return 0;
+}
+
+int check_timeline_args(fit_ctx* c, int32_t slots, int32_t slot_min) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
+    if (slots < 1 || slots > TL_MAX_SLOTS || slot_min < 1)
+        return fail(FIT_E_INVAL, "horizon of %d slots x %d min (1..%d slots)", slots, slot_min,
+                    TL_MAX_SLOTS);
+    if (c->nn > (int32_t)TL_POS_MASK + 1)
+        return fail(FIT_E_INVAL, "%d nodes exceed the timeline key's %d-bit position", c->nn,
+                    TL_POS_BITS);
     return 0;
 }
 
@@ -866,6 +1063,143 @@ int fit_partition_free(fit_ctx* c, int32_t p, int64_t* cpu, int64_t* mem, int64_
     *mem = sm;
     *gpu = sg;
     return 0;
+}
+
+int fit_load_timeline(fit_ctx* c, int32_t slots, int32_t slot_min, const int32_t* rel_off,
+                      const int32_t* rel_slot, const int32_t* rel_cpu, const int32_t* rel_mem,
+                      const int32_t* rel_gpu) {
+    int rc = check_timeline_args(c, slots, slot_min);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    int64_t ne = 0;
+    if (rel_off) {
+        if (rel_off[0] != 0) return fail(FIT_E_INVAL, "rel_off[0] must be 0");
+        for (int32_t x = 0; x < c->n; ++x)
+            if (rel_off[x + 1] < rel_off[x]) return fail(FIT_E_INVAL, "rel_off decreases at %d", x);
+        ne = rel_off[c->n];
+        if (ne > 0 && (!rel_slot || !rel_cpu || !rel_mem || !rel_gpu))
+            return fail(FIT_E_INVAL, "null release arrays");
+    }
+    if (c->rel_off.ensure(c->n + 1) || c->rel_slot.ensure(std::max<int64_t>(ne, 1)) ||
+        c->rel_cpu.ensure(std::max<int64_t>(ne, 1)) || c->rel_mem.ensure(std::max<int64_t>(ne, 1)) ||
+        c->rel_gpu.ensure(std::max<int64_t>(ne, 1)))
+        return FIT_E_OOM;
+    if (rel_off) {
+        HIP_TRY(hipMemcpyAsync(c->rel_off.p, rel_off, sizeof(int32_t) * (c->n + 1),
+                               hipMemcpyHostToDevice, c->st));
+        if (ne > 0) {
+            const size_t b = sizeof(int32_t) * ne;
+            HIP_TRY(hipMemcpyAsync(c->rel_slot.p, rel_slot, b, hipMemcpyHostToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_cpu.p, rel_cpu, b, hipMemcpyHostToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_mem.p, rel_mem, b, hipMemcpyHostToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_gpu.p, rel_gpu, b, hipMemcpyHostToDevice, c->st));
+        }
+    }
+    return load_timeline_impl(c, slots, slot_min, rel_off ? ne : -1);
+}
+
+int fit_load_timeline_device(fit_ctx* c, int32_t slots, int32_t slot_min, const int32_t* rel_off,
+                             int64_t n_rel, const int32_t* rel_slot, const int32_t* rel_cpu,
+                             const int32_t* rel_mem, const int32_t* rel_gpu) {
+    int rc = check_timeline_args(c, slots, slot_min);
+    if (rc) return rc;
+    if (n_rel < 0 || (n_rel > 0 && (!rel_off || !rel_slot || !rel_cpu || !rel_mem || !rel_gpu)))
+        return fail(FIT_E_INVAL, "bad release arrays");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->rel_off.ensure(c->n + 1) || c->rel_slot.ensure(std::max<int64_t>(n_rel, 1)) ||
+        c->rel_cpu.ensure(std::max<int64_t>(n_rel, 1)) ||
+        c->rel_mem.ensure(std::max<int64_t>(n_rel, 1)) || c->rel_gpu.ensure(std::max<int64_t>(n_rel, 1)))
+        return FIT_E_OOM;
+    if (rel_off) {
+        HIP_TRY(hipMemcpyAsync(c->rel_off.p, rel_off, sizeof(int32_t) * (c->n + 1),
+                               hipMemcpyDeviceToDevice, c->st));
+        if (n_rel > 0) {
+            const size_t b = sizeof(int32_t) * n_rel;
+            HIP_TRY(hipMemcpyAsync(c->rel_slot.p, rel_slot, b, hipMemcpyDeviceToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_cpu.p, rel_cpu, b, hipMemcpyDeviceToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_mem.p, rel_mem, b, hipMemcpyDeviceToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->rel_gpu.p, rel_gpu, b, hipMemcpyDeviceToDevice, c->st));
+        }
+    }
+    return load_timeline_impl(c, slots, slot_min, rel_off ? n_rel : -1);
+}
+
+static int check_place_tl_args(fit_ctx* c, int32_t j, const void* a, const void* b,
+                               const void* d, const void* e, const void* f, const void* out,
+                               const void* outs) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
+    if (!c->have_tl) return fail(FIT_E_STATE, "fit_load_timeline not called");
+    if (j < 0 || (j > 0 && (!a || !b || !d || !e || !f || !out || !outs)))
+        return fail(FIT_E_INVAL, "bad job arrays");
+    return 0;
+}
+
+int fit_place_tl(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem,
+                 const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out_node,
+                 int32_t* out_start, fit_stats* stats) {
+    int rc = check_place_tl_args(c, j, cpu, mem, gpu, wall, part, out_node, out_start);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    for (int32_t q = 0; q < j; ++q)
+        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0)
+            return fail(FIT_E_INVAL, "job %d: negative demand", q);
+    size_t m = std::max(j, 1);
+    if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
+        c->jpart.ensure(m) || c->out.ensure(m) || c->outs.ensure(m))
+        return FIT_E_OOM;
+    const size_t b = sizeof(int32_t) * j;
+    HIP_TRY(hipMemcpyAsync(c->jcpu.p, cpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jmem.p, mem, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jgpu.p, gpu, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jwall.p, wall, b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->jpart.p, part, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
+    rc = place_tl_impl(c, j, c->jcpu.p, c->jmem.p, c->jgpu.p, c->jwall.p, c->jpart.p, c->out.p,
+                       c->outs.p, stats);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_node, c->out.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(out_start, c->outs.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int fit_place_tl_device(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem,
+                        const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                        int32_t* out_node, int32_t* out_start, fit_stats* stats) {
+    int rc = check_place_tl_args(c, j, cpu, mem, gpu, wall, part, out_node, out_start);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    rc = place_tl_impl(c, j, cpu, mem, gpu, wall, part, out_node, out_start, stats);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int fit_read_timeline(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_tl) return fail(FIT_E_STATE, "fit_load_timeline not called");
+    if (c->n > 0 && (!cpu || !mem || !gpu)) return fail(FIT_E_INVAL, "null output");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t cells = (size_t)c->n * c->tl_slots;
+    DBuf<int32_t> d[3];
+    for (auto& x : d)
+        if (x.ensure(std::max<size_t>(cells, 1))) {
+            for (auto& y : d) y.release();
+            return FIT_E_OOM;
+        }
+    // rows of nodes outside every partition (mask 0) are not on the device: -1, like unusable
+    int rc = 0;
+    for (auto& x : d)
+        if (hipMemsetAsync(x.p, 0xff, sizeof(int32_t) * cells, c->st) != hipSuccess) rc = FIT_E_HIP;
+    if (rc || launch_expand_tl(c->st, c->rec.p, c->slab.p, c->segcnt.p, c->nn, c->tl_slots, d[0].p,
+                         d[1].p, d[2].p) != hipSuccess ||
+        hipMemcpyAsync(cpu, d[0].p, sizeof(int32_t) * cells, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipMemcpyAsync(mem, d[1].p, sizeof(int32_t) * cells, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipMemcpyAsync(gpu, d[2].p, sizeof(int32_t) * cells, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess)
+        rc = fail(FIT_E_HIP, "timeline read-back failed");
+    for (auto& x : d) x.release();
+    return rc;
 }
 
 }  // extern "C"

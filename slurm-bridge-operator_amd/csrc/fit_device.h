@@ -59,6 +59,18 @@ struct CompOut {
     int64_t t_commit, t_wait;  // 100 MHz realtime ticks spent committing / waiting for scans
 };
 
+// ---- SPEC §2b time-windowed backfill (fit_timeline.hip) --------------------
+constexpr int TL_MAX_SLOTS = 1024;  // horizon limit (slots); the C5 horizon
+constexpr int TL_UCAP = 64;         // dirty nodes per component per round (one per lane)
+constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position
+constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;
+
+// One run of equal free resources on a node's timeline: slots [previous end, end).  A node's
+// list is canonical (adjacent runs differ) and ends at the horizon; at most TL_MAX_SLOTS runs.
+struct alignas(16) Seg {
+    int32_t end, cpu, mem, gpu;
+};
+
 struct CommitResult {
     int32_t done;   // jobs resolved this round (prefix of the window)
     int32_t stop;   // 0 window exhausted, 1 candidate list ran out, 2 dirty set full

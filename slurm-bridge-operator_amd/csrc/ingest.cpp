@@ -5,6 +5,7 @@
 // returns FIT_E_PARSE.  Text is handled as ASCII (scontrol output is ASCII).
 #include <cstdint>
 #include <cstring>
+#include <string>
 #include <string_view>
 #include <vector>
 
@@ -388,6 +389,196 @@ void fit_partition_capacity(const fit_node* nodes, int32_t n, int64_t* cpu, int6
     if (memory) *memory = (int64_t)(m * (2u << 10));  // node.go:193 — MiB × 2048, as the ref
     if (gpu) *gpu = (int64_t)g;
     if (pods) *pods = (int64_t)c;  // node.go:197
+}
+
+// ---------------------------------------------------------------- node-table ingest (f3)
+// the Client.Nodes record loop + parseNode (slurm.go:354-363, parse.go:291-308)
+// extended with the fields the reference drops — NodeName, Gres / GresUsed (a1: Gpus and AlloGpus
+// are never set there), State and Partitions — straight into the engine's SoA columns, and Slurm
+// hostlist expansion (a3: parsePartition splits "node[1-3,5]" into "node[1-3" and "5]").
+
+}  // extern "C"
+
+namespace {
+
+// Split on `sep` outside parentheses / brackets ("gpu:4(S:0,1),mps:100" → 2 items).
+std::vector<sv> split_top(sv s, char sep) {
+    std::vector<sv> out;
+    int depth = 0;
+    size_t b = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+        const char ch = s[i];
+        if (ch == '(' || ch == '[') ++depth;
+        else if ((ch == ')' || ch == ']') && depth > 0) --depth;
+        else if (ch == sep && depth == 0) {
+            out.push_back(s.substr(b, i - b));
+            b = i + 1;
+        }
+    }
+    out.push_back(s.substr(b));
+    return out;
+}
+
+// Σ of the counts of "gpu" entries of a Gres / GresUsed value: name[:type]:count[(...)], count
+// with an optional K/M/G multiplier (Slurm's suffixes), "(null)" = none.  -1: malformed count.
+int64_t gres_gpus(sv v) {
+    int64_t total = 0;
+    for (sv item : split_top(v, ',')) {
+        const size_t paren = item.find('(');
+        if (paren != sv::npos) item = item.substr(0, paren);
+        if (item.substr(0, 3) != "gpu" || (item.size() > 3 && item[3] != ':')) continue;
+        const std::vector<sv> parts = split(item, ":");
+        if (parts.size() < 2) {  // bare "gpu": one
+            total += 1;
+            continue;
+        }
+        sv cnt = parts.back();
+        int64_t mul = 1;
+        if (!cnt.empty() && (cnt.back() == 'K' || cnt.back() == 'M' || cnt.back() == 'G')) {
+            mul = cnt.back() == 'K' ? 1024 : cnt.back() == 'M' ? 1024 * 1024 : 1024 * 1024 * 1024;
+            cnt.remove_suffix(1);
+        }
+        int64_t c;
+        if (parse_int(cnt, c) != 0) {
+            if (parts.size() == 2) {  // "gpu:a100" (type, no count): one
+                total += 1;
+                continue;
+            }
+            return -1;
+        }
+        total += c * mul;
+    }
+    return total;
+}
+
+// A node takes new work unless a State token says otherwise (DOWN*, IDLE+DRAIN, ...); the flags
+// follow `scontrol show node` (base state + '+'-joined flags, '*' = not responding).
+bool state_schedulable(sv v) {
+    if (v.empty()) return true;
+    if (v.find('*') != sv::npos) return false;  // not responding
+    for (sv tok : split(v, "+")) {
+        while (!tok.empty() && strchr("~#!%$@^-", tok.back())) tok.remove_suffix(1);
+        static const char* const bad[] = {"DOWN",     "DRAIN",         "DRAINED",      "DRAINING",
+                                          "FAIL",     "FAILING",       "FUTURE",       "MAINT",
+                                          "POWERED_DOWN", "POWER_DOWN", "POWERING_DOWN",
+                                          "REBOOT_ISSUED", "REBOOT_REQUESTED", "INVAL", "UNKNOWN",
+                                          "NOT_RESPONDING"};
+        for (const char* b : bad)
+            if (tok == b) return false;
+    }
+    return true;
+}
+
+int32_t to_i32(int64_t v) {
+    return v > INT32_MAX ? INT32_MAX : v < INT32_MIN ? INT32_MIN : (int32_t)v;
+}
+
+// One bracket group "01-03,7" → the numbers as strings, zero padded to the width of the lower
+// bound when it has a leading zero (Slurm hostlist).  false: malformed.
+bool expand_ranges(sv body, std::vector<std::string>& out) {
+    for (sv r : split(body, ",")) {
+        const size_t dash = r.find('-');
+        sv lo = dash == sv::npos ? r : r.substr(0, dash), hi = dash == sv::npos ? r : r.substr(dash + 1);
+        int64_t a, b;
+        if (lo.empty() || hi.empty() || lo[0] == '-' || lo[0] == '+' || hi[0] == '-' || hi[0] == '+' ||
+            parse_int(lo, a) || parse_int(hi, b) || b < a || b - a > 1000000)
+            return false;
+        const size_t width = (lo.size() > 1 && lo[0] == '0') ? lo.size() : 0;
+        for (int64_t x = a; x <= b; ++x) {
+            std::string d = std::to_string(x);
+            if (d.size() < width) d.insert(0, width - d.size(), '0');
+            out.push_back(std::move(d));
+        }
+    }
+    return true;
+}
+
+// One hostlist item (no top-level comma): prefix[r]mid[r]...suffix → cartesian expansion.
+bool expand_item(sv item, std::vector<std::string>& out) {
+    std::vector<std::string> acc{std::string()};
+    size_t i = 0;
+    while (i < item.size()) {
+        const size_t lb = item.find('[', i);
+        if (lb == sv::npos) {
+            for (auto& a : acc) a.append(item.substr(i));
+            break;
+        }
+        const size_t rb = item.find(']', lb);
+        if (rb == sv::npos) return false;
+        for (auto& a : acc) a.append(item.substr(i, lb - i));
+        std::vector<std::string> nums;
+        if (!expand_ranges(item.substr(lb + 1, rb - lb - 1), nums)) return false;
+        std::vector<std::string> next;
+        next.reserve(acc.size() * nums.size());
+        for (auto& a : acc)
+            for (auto& n : nums) next.push_back(a + n);
+        acc.swap(next);
+        i = rb + 1;
+    }
+    for (auto& a : acc)
+        if (!a.empty()) out.push_back(std::move(a));
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen) {
+    if (!expr || !buf || buflen < 0) return FIT_E_INVAL;
+    std::vector<std::string> names;
+    for (sv item : split_top(trim_space(sv(expr)), ','))
+        if (!item.empty() && !expand_item(item, names)) return FIT_E_PARSE;
+    std::vector<sv> views(names.begin(), names.end());
+    return put_names(views, buf, buflen);
+}
+
+int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32_t cap,
+                     int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free, int32_t* avail_min,
+                     uint32_t* part_mask, char* names, int32_t names_len) {
+    if (!text || cap < 0 || np < 0 || np > FIT_MAX_PARTITIONS || (np > 0 && !partitions) ||
+        (cap > 0 && (!cpu_free || !mem_free || !gpu_free || !avail_min || !part_mask)))
+        return FIT_E_INVAL;
+    std::vector<sv> pnames;
+    for (const char* p = partitions; (int32_t)pnames.size() < np; p += strlen(p) + 1) pnames.push_back(p);
+    std::vector<sv> node_names;
+    int32_t n = 0;
+    for (sv rec : split(trim_space(sv(text)), "\n\n")) {  // Client.Nodes, slurm.go:354-363
+        if (rec.empty()) continue;
+        if (n == cap) return FIT_E_INVAL;
+        fit_node base;
+        parse_node(rec, base);  // CPUTot / CPUAlloc / RealMemory / AllocMem exactly as parseNode
+        sv name, state;
+        int64_t gpus = 0, used = 0;
+        uint32_t mask = 0;
+        for (sv f : fields(rec)) {
+            const std::vector<sv> kv = split(f, "=");
+            if (kv.size() != 2) continue;  // same key rule as parseNode (parse.go:294)
+            if (kv[0] == "NodeName") name = kv[1];
+            else if (kv[0] == "State") state = kv[1];
+            else if (kv[0] == "Gres" || kv[0] == "GresUsed") {
+                const int64_t g = gres_gpus(kv[1]);
+                if (g < 0) return FIT_E_PARSE;
+                (kv[0] == "Gres" ? gpus : used) = g;
+            } else if (kv[0] == "Partitions") {
+                for (sv pn : split(kv[1], ","))
+                    for (int32_t p = 0; p < np; ++p)
+                        if (pnames[p] == pn) mask |= 1u << p;
+            }
+        }
+        cpu_free[n] = to_i32(base.cpus - base.allo_cpus);
+        mem_free[n] = to_i32(base.memory - base.allo_memory);
+        gpu_free[n] = to_i32(gpus - used);
+        avail_min[n] = INT32_MAX;  // no horizon in `scontrol show nodes`; reservations set it
+        part_mask[n] = state_schedulable(state) ? mask : 0u;
+        node_names.push_back(name);
+        ++n;
+    }
+    if (names) {
+        const int rc = put_names(node_names, names, names_len);
+        if (rc < 0) return rc;
+    }
+    return n;
 }
 
 }  // extern "C"

@@ -34,7 +34,7 @@ __all__ = [
     "parse_partition", "parse_partitions_names", "extract_batch_resources", "apply_spec",
     "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
     "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
-    "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS",
+    "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS", "expand_hostlist", "ingest_nodes",
 ]
 
 
@@ -106,6 +106,40 @@ def parse_partition(text: str) -> list[str]:
 
 def parse_partitions_names(text: str) -> list[str]:
     return _names(lib().fit_parse_partitions_names, text)
+
+
+def expand_hostlist(expr: str) -> list[str]:
+    """Slurm hostlist expansion (fixes parsePartition's split, parse.go:278-289)."""
+    buflen = 1 << 16
+    while True:
+        buf = C.create_string_buffer(buflen)
+        n = lib().fit_expand_hostlist(expr.encode(), buf, buflen)
+        if n == FIT_E_PARSE:
+            raise ValueError(f"malformed hostlist {expr!r}")
+        if n >= 0:
+            return [x.decode() for x in buf.raw.split(b"\0")[:n]]
+        if buflen > 1 << 28:
+            check(n, "fit_expand_hostlist")
+        buflen *= 16
+
+
+def ingest_nodes(text: str, partitions: list[str]):
+    """`scontrol show nodes` text → (synth.Nodes columns for Engine.load_nodes, node names)
+    (Client.Nodes + parseNode, slurm.go:354-363 / parse.go:291-308, plus Gres,
+    GresUsed, State, Partitions, NodeName)."""
+    from .synth import Nodes
+    cap = text.count("\n\n") + 2
+    cols = [np.empty(cap, np.int32) for _ in range(4)] + [np.empty(cap, np.uint32)]
+    blob = b"".join(p.encode() + b"\0" for p in partitions)
+    names_len = len(text.encode()) + 64
+    names = C.create_string_buffer(names_len)
+    n = lib().fit_ingest_nodes(text.encode(), blob, len(partitions), cap, *[_ptr(c) for c in cols], names,
+                               names_len)
+    if n == FIT_E_PARSE:
+        raise ValueError("malformed Gres count")
+    check(n, "fit_ingest_nodes")
+    nodes = Nodes(*(c[:n].copy() for c in cols))
+    return nodes, [x.decode() for x in names.raw.split(b"\0")[:n]]
 
 
 @dataclass
@@ -290,6 +324,45 @@ class Engine:
                                      _ptr(part), _ptr(nodes_k) if nodes_k is not None else None, kmax,
                                      _ptr(out), C.byref(st)), "fit_place_device")
         return st.as_dict()
+
+    # ---- time-windowed backfill ------------------------------------------
+    def load_timeline(self, tline):
+        """Release events (synth.Timeline) over a horizon of tline.slots slots of tline.slot_min
+        minutes, on top of the node table of the last load_nodes."""
+        cols = [np.ascontiguousarray(a, np.int32) for a in (tline.off, tline.slot, tline.cpu, tline.mem,
+                                                            tline.gpu)]
+        check(lib().fit_load_timeline(self._h, int(tline.slots), int(tline.slot_min), *[_ptr(c) for c in cols]),
+              "fit_load_timeline")
+        self.slots = int(tline.slots)
+
+    def load_timeline_device(self, slots, slot_min, off, slot, cpu, mem, gpu):
+        """torch int32 tensors on this GPU (off has n + 1 entries)."""
+        check(lib().fit_load_timeline_device(self._h, int(slots), int(slot_min), _ptr(off), int(slot.numel()),
+                                             *[_ptr(t) for t in (slot, cpu, mem, gpu)]), "fit_load_timeline_device")
+        self.slots = int(slots)
+
+    def place_tl(self, jobs):
+        """Returns (node[J], start_slot[J], stats)."""
+        cols = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
+        part = np.ascontiguousarray(jobs.part, np.uint16)
+        j = len(part)
+        node, start = np.empty(j, np.int32), np.empty(j, np.int32)
+        st = FitStats()
+        check(lib().fit_place_tl(self._h, j, *[_ptr(c) for c in cols], _ptr(part), _ptr(node), _ptr(start),
+                                 C.byref(st)), "fit_place_tl")
+        return node, start, st.as_dict()
+
+    def place_tl_device(self, cpu, mem, gpu, wall, part, out_node, out_start):
+        st = FitStats()
+        check(lib().fit_place_tl_device(self._h, int(cpu.numel()), *[_ptr(t) for t in (cpu, mem, gpu, wall, part)],
+                                        _ptr(out_node), _ptr(out_start), C.byref(st)), "fit_place_tl_device")
+        return st.as_dict()
+
+    def read_timeline(self):
+        """Dense [n, slots, 3] int32 (cpu, mem, gpu)."""
+        c, m, g = (np.empty((self.n, self.slots), np.int32) for _ in range(3))
+        check(lib().fit_read_timeline(self._h, _ptr(c), _ptr(m), _ptr(g)), "fit_read_timeline")
+        return np.stack([c, m, g], axis=2)
 
     def read_nodes(self):
         c, m, g = (np.empty(self.n, np.int32) for _ in range(3))

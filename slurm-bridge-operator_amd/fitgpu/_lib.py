@@ -31,6 +31,8 @@ EXPORTS = [
     "fit_parse_duration", "fit_parse_resources", "fit_parse_nodes", "fit_parse_partition",
     "fit_parse_partitions_names", "fit_extract_batch_resources", "fit_apply_spec", "fit_array_len",
     "fit_pod_request", "fit_job_demand", "fit_partition_capacity",
+    "fit_load_timeline", "fit_load_timeline_device", "fit_place_tl", "fit_place_tl_device",
+    "fit_read_timeline", "fit_ingest_nodes", "fit_expand_hostlist",
 ]
 
 
@@ -100,6 +102,13 @@ def lib() -> C.CDLL:
         for name in ("fit_place", "fit_place_device"):
             getattr(L, name).argtypes = [P, i32, P, P, P, P, P, P, i32, P, C.POINTER(FitStats)]
         L.fit_read_nodes.argtypes = [P, P, P, P]
+        L.fit_load_timeline.argtypes = [P, i32, i32, P, P, P, P, P]
+        L.fit_load_timeline_device.argtypes = [P, i32, i32, P, i64, P, P, P, P]
+        for name in ("fit_place_tl", "fit_place_tl_device"):
+            getattr(L, name).argtypes = [P, i32, P, P, P, P, P, P, P, C.POINTER(FitStats)]
+        L.fit_read_timeline.argtypes = [P, P, P, P]
+        L.fit_ingest_nodes.argtypes = [C.c_char_p, C.c_char_p, i32, i32, P, P, P, P, P, C.c_char_p, i32]
+        L.fit_expand_hostlist.argtypes = [C.c_char_p, C.c_char_p, i32]
         L.fit_partition_free.argtypes = [P, i32, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
         L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]

@@ -26,6 +26,7 @@ SEEDS = {"c1": 0x5EED0001, "c2": 0x5EED0002, "c3": 0x5EED0003, "c4": 0x5EED0004,
 
 # stream ids (never reuse one across fields)
 S_NCLASS, S_NMEM, S_NGPU, S_ACPU, S_AMEM, S_AGPU, S_NPART, S_AVF, S_AVV = range(0, 9)
+S_RN, S_RS = 9, 10  # C5: running jobs per node, their release slots
 S_JCPU, S_JMEM, S_JGPUF, S_JGPUV, S_JWO, S_JWV, S_JPART, S_JK = range(16, 24)
 S_PTIME = 32
 
@@ -87,6 +88,21 @@ class Jobs:
 
 
 @dataclass
+class Timeline:
+    """C5 reservation horizon: ``slots`` slots of ``slot_min`` minutes, plus the
+    release events of the jobs already running on each node, CSR by node id: events of node x are
+    [off[x], off[x+1]), slots non-decreasing; at slot ``slot[e]`` the node gets back
+    (cpu[e], mem[e], gpu[e])."""
+    slots: int
+    slot_min: int
+    off: np.ndarray  # int32 [n + 1]
+    slot: np.ndarray  # int32 [E]
+    cpu: np.ndarray  # int32 [E]
+    mem: np.ndarray  # int32 [E], MiB
+    gpu: np.ndarray  # int32 [E]
+
+
+@dataclass
 class Partitions:
     max_time_min: np.ndarray  # int32, -1 unlimited
     max_cpus_per_node: np.ndarray  # int32, -1 unlimited
@@ -120,6 +136,39 @@ def gen_nodes(seed: int, n: int, parts: int, gpu_heavy: bool = False, start: int
         avail_min=avail.astype(np.int32),
         part_mask=(np.uint32(1) << part.astype(np.uint32)).astype(np.uint32),
     )
+
+
+def gen_releases(seed: int, n: int, slots: int = 1024, slot_min: int = 5, gpu_heavy: bool = False,
+                 start: int = 0) -> Timeline:
+    """Release events of the allocation gen_nodes() subtracts: node x runs R = 1..4 jobs (uniform)
+    that hold the allocated (cpu, mem, gpu) in R near-equal integer parts, each released at a
+    uniform slot in [1, slots)."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    cpus = NODE_CPUS[uni(rnd(seed, S_NCLASS, i), 6)]
+    mem = cpus * NODE_MEMMUL[uni(rnd(seed, S_NMEM, i), 3)]
+    if gpu_heavy:
+        gpus = np.full(n, 8, dtype=np.int64)
+    else:
+        u = uni(rnd(seed, S_NGPU, i), 100)
+        gpus = np.where(u < 70, 0, np.where(u < 85, 4, 8)).astype(np.int64)
+    alloc = np.stack([cpus * uni(rnd(seed, S_ACPU, i), 51) // 100, mem * uni(rnd(seed, S_AMEM, i), 51) // 100,
+                      gpus * uni(rnd(seed, S_AGPU, i), 51) // 100], axis=1)  # [n, 3]
+    r = 1 + uni(rnd(seed, S_RN, i), 4)  # [n]
+    rr = np.arange(4, dtype=np.int64)
+    idx = (i[:, None] * np.uint64(4) + rr[None, :].astype(np.uint64))
+    rs = 1 + uni(rnd(seed, S_RS, idx), slots - 1)  # [n, 4]
+    rs = np.where(rr[None, :] < r[:, None], rs, np.iinfo(np.int64).max)
+    rs.sort(axis=1)
+    # part k of R: alloc*(k+1)//R - alloc*k//R
+    k = rr[None, :, None]
+    part = alloc[:, None, :] * (k + 1) // r[:, None, None] - alloc[:, None, :] * k // r[:, None, None]
+    valid = rr[None, :] < r[:, None]
+    counts = valid.sum(axis=1)
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(counts)
+    return Timeline(slots=slots, slot_min=slot_min, off=off.astype(np.int32),
+                    slot=rs[valid].astype(np.int32), cpu=part[..., 0][valid].astype(np.int32),
+                    mem=part[..., 1][valid].astype(np.int32), gpu=part[..., 2][valid].astype(np.int32))
 
 
 def gen_jobs(seed: int, j: int, parts: int, multi_node: bool = False, start: int = 0) -> Jobs:
@@ -161,7 +210,9 @@ CONFIGS = {
     "c2": (4096, 65536, 1, False, False),
     "c3": (100_000, 1_000_000, 16, False, False),
     "c4": (100_000, 1_000_000, 16, True, True),
+    "c5": (100_000, 1_000_000, 16, False, False),  # + 1,024-slot horizon (make_c5)
 }
+C5_SLOTS, C5_SLOT_MIN = 1024, 5  # 1,024 slots × 5 min = 85.3 h ≥ the longest walltime (2,880 min)
 
 
 def make_config(name: str, nodes: int | None = None, jobs: int | None = None):
@@ -171,6 +222,17 @@ def make_config(name: str, nodes: int | None = None, jobs: int | None = None):
     n = n if nodes is None else nodes
     j = j if jobs is None else jobs
     return gen_nodes(seed, n, p, gh), gen_jobs(seed, j, p, mn), gen_partitions(seed, p)
+
+
+def make_c5(nodes: int | None = None, jobs: int | None = None):
+    """C5 (BASELINE.json config 5): C3's cluster shape plus the release timeline of the running
+    jobs over a 1,024-slot horizon.  Returns (nodes, timeline, jobs, partitions)."""
+    n, j, p, gh, mn = CONFIGS["c5"]
+    seed = SEEDS["c5"]
+    n = n if nodes is None else nodes
+    j = j if jobs is None else jobs
+    return (gen_nodes(seed, n, p, gh), gen_releases(seed, n, C5_SLOTS, C5_SLOT_MIN, gh),
+            gen_jobs(seed, j, p, mn), gen_partitions(seed, p))
 
 
 def make_c1():
