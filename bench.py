@@ -1,6 +1,12 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json's headline metric on MI355X: placements/sec (+ job×node fit evals/sec)
-at 100k nodes × 1M jobs (config C3, 16 partitions), node-sharded over N GPUs.
+at 100k nodes × 1M jobs (config C3, 16 partitions) per GPU.
+
+N > 1 (default --scaling weak, SURVEY §8 e / DESIGN §3.5): the placement path partitions into
+independent partition components, so each rank places its own 100k × 1M cluster shard (a
+disjoint slice of the generator streams) with no collective in the data path; `value` is the
+aggregate placements/s of all ranks.  --scaling strong splits ONE 100k × 1M placement over the
+ranks instead (--shard-mode components | nodes: RCCL allgather + u64 min-allreduce per round).
 
 A "step" is one complete placement of the 1M-job stream against a freshly loaded 100k-node table:
 fit_load_nodes_device (from HBM-resident columns) + fit_place_device.  Inputs are synthetic
@@ -84,10 +90,16 @@ def parse_args():
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="jobs in the CPU baseline sample (default 40,000; c5: 3,000)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="test only: every rank on cuda:0 with gloo (rehearse N>1 on a 1-GPU box)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/gpu_pmc.sh + tools/pmc_json.py) with HBM bytes/launch")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = every rank places its own 100k x 1M cluster shard (independent "
+                         "partition components, no data-path collective); strong = one 100k x 1M "
+                         "placement split over the ranks (--shard-mode)")
     ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
-                    help="N>1 split: auto = partition components when there are >= N of them")
+                    help="strong scaling split: auto = partition components when there are >= N of them")
     return ap.parse_args()
 
 
@@ -105,21 +117,30 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if a.rehearse:
+        local = 0
+        if a.scaling != "weak":
+            raise SystemExit("--rehearse supports --scaling weak only")
     torch.cuda.set_device(local)
+    weak = world > 1 and a.scaling == "weak"
+    nid = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        obj = [nccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        nid = obj[0]
-    else:
-        nid = None
+        if a.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if not weak:
+            obj = [nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            nid = obj[0]
+    shard = rank if weak else 0  # weak: this rank's own cluster shard (disjoint generator slice)
 
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
     tl = a.workload == "c5"
     if tl:
-        nodes, tline, jobs, parts = synth.make_c5()
+        nodes, tline, jobs, parts = synth.make_c5(shard=shard)
     else:
-        nodes, jobs, parts = synth.make_config(a.workload)
+        nodes, jobs, parts = synth.make_config(a.workload, shard=shard)
     dev = torch.device("cuda", local)
     T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
     d_nodes = [T(nodes.cpu_free), T(nodes.mem_free), T(nodes.gpu_free), T(nodes.avail_min),
@@ -132,7 +153,10 @@ def main():
         d_start = torch.empty(jobs.j, dtype=torch.int32, device=dev)
 
     mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
-    eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
+    if weak:
+        eng = Engine(device=local)  # independent shard: no collective in the data path
+    else:
+        eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
     eng.load_partitions(parts)
 
     def step():
@@ -155,8 +179,9 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    cdev = torch.device("cpu") if a.rehearse else dev  # gloo reduces CPU tensors
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
@@ -164,16 +189,18 @@ def main():
     s0 = stats[-1]
     assert s0["placed"] + s0["unplaced"] + s0["rejected"] == jobs.j
 
-    value = jobs.j * a.steps / el
+    value = jobs.j * a.steps / el * (world if weak else 1)
     agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan", "ms_commit",
                                                   "ms_exchange", "ms_device", "placed", "unplaced")}
     evals_local = agg["evals"]
-    if world > 1:  # performed evaluations summed over ranks (each rank scanned its own share)
-        t = torch.tensor([float(agg["evals"])], dtype=torch.float64, device=dev)
+    if world > 1:  # performed / useful evaluations summed over ranks
+        t = torch.tensor([float(agg["evals"]), float(agg["useful_evals"])], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
-        agg["evals"] = int(t.item())
+        agg["evals"], agg["useful_evals"] = int(t[0].item()), int(t[1].item())
     used_mode = {0: "1 GPU", 1: f"node-sharded x{world} (RCCL allgather + u64 min-allreduce per round)",
                  2: f"partition-component-sharded x{world} (one RCCL merge)"}[stats[-1]["shard_mode"]]
+    if weak:
+        used_mode = f"{world} independent cluster shards (one per GPU, no data-path collective)"
     kernels = kernel_table(agg, stats, a.steps, world, evals_local,
                            ("k_scan_tl", "k_commit_tl") if tl else ("k_scan", "k_commit"))
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_launch"] * kernels[k]["launches"])
@@ -207,9 +234,11 @@ def main():
     line = {
         "metric": base["metric"], "value": round(value, 1), "unit": "placements/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "higher_is_better": True, "scaling": "weak" if (weak or world == 1) else "strong", "vs_baseline": None, "dtype": "int32",
         "data": "synthetic (splitmix64 generator, fitgpu/synth.py; DESIGN.md §5)",
-        "config": {"workload": a.workload, "nodes": nodes.n, "jobs": jobs.j, "partitions": parts.p,
+        "config": {"workload": a.workload, "nodes": nodes.n * (world if weak else 1),
+                   "jobs": jobs.j * (world if weak else 1), "partitions": parts.p * (world if weak else 1),
+                   "per_gpu": {"nodes": nodes.n, "jobs": jobs.j} if weak else None,
                    **({"slots": tline.slots, "slot_min": tline.slot_min} if tl else {}),
                    "parallelism": used_mode, "components": stats[-1]["components"]},
         "fit_evals_per_s": {"useful": round(agg["useful_evals"] / el, 1), "performed": round(agg["evals"] / el, 1)},

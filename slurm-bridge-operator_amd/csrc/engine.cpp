@@ -51,24 +51,26 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk);
 // time-windowed backfill (fit_timeline.hip)
 hipError_t launch_build_tl(hipStream_t st, const int32_t* cpu, const int32_t* mem,
-                           const int32_t* gpu, const int32_t* av, const int32_t* perm,
-                           int32_t nn, int32_t H, int32_t slot_min, const int32_t* off,
-                           const int32_t* rs, const int32_t* rc, const int32_t* rm,
-                           const int32_t* rg, Seg* slab, int32_t* segcnt, uint32_t* err);
-hipError_t launch_scan_tl(int blocks, hipStream_t st, const NodeRec* rec, const Seg* slab,
-                          const int32_t* segcnt, const int32_t* jl, const int32_t* jcpu,
-                          const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
-                          const uint16_t* jpart, const CompPlan* plan, int ncomp, uint64_t* cand,
-                          uint64_t* bnd, JobRec* wjob, int32_t H, int32_t slot_min);
+                           const int32_t* gpu, const int32_t* av, const uint32_t* mask,
+                           const int32_t* perm, int32_t nn, int32_t H, int32_t slot_min,
+                           const int32_t* off, const int32_t* rs, const int32_t* rc,
+                           const int32_t* rm, const int32_t* rg, Seg* slab, TlHdr* hdr,
+                           uint32_t* err);
+hipError_t launch_scan_tl(int blocks, hipStream_t st, const Seg* slab, const TlHdr* hdr,
+                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
+                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                          const CompPlan* plan, int ncomp, uint64_t* cand, uint64_t* bnd,
+                          JobRec* wjob, int32_t H, int32_t slot_min);
 size_t commit_tl_lds_bytes(int32_t max_component_nodes);
-hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, const NodeRec* rec,
-                            Seg* slab, int32_t* segcnt, const CompPlan* plan,
-                            const uint64_t* cand, int64_t rank_stride, int nranks,
-                            const uint64_t* bnd, const JobRec* wjob, int32_t* out, int32_t* outs,
-                            CommitResult* res, int32_t H);
-hipError_t launch_expand_tl(hipStream_t st, const NodeRec* rec, const Seg* slab,
-                            const int32_t* segcnt, int32_t nn, int32_t H, int32_t* oc,
-                            int32_t* om, int32_t* og);
+int commit_tl_runs(int32_t max_component_nodes);
+hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg* slab,
+                            TlHdr* hdr, const CompPlan* plan, const uint64_t* cand,
+                            int64_t rank_stride, int nranks, const uint64_t* bnd,
+                            const JobRec* wjob, const int32_t* perm, int32_t* out, int32_t* outs,
+                            CommitResult* res, int32_t H, int32_t R);
+hipError_t launch_expand_tl(hipStream_t st, const int32_t* perm, const Seg* slab,
+                            const TlHdr* hdr, int32_t nn, int32_t H, int32_t* oc, int32_t* om,
+                            int32_t* og);
 }  // namespace fitgpu
 
 using namespace fitgpu;
@@ -222,7 +224,8 @@ struct fit_ctx {
     int32_t tl_slots = 0, tl_slot_min = 0;
     bool have_tl = false;
     DBuf<Seg> slab;
-    DBuf<int32_t> segcnt, outs, rel_off, rel_slot, rel_cpu, rel_mem, rel_gpu;
+    DBuf<TlHdr> tlhdr;
+    DBuf<int32_t> outs, rel_off, rel_slot, rel_cpu, rel_mem, rel_gpu;
     DBuf<uint32_t> tl_err;
     HBuf<uint32_t> h_tl_err;
 
@@ -231,7 +234,8 @@ struct fit_ctx {
                         &jwall, &out, &jl, &jpk})
             b->release();
         rec.release();
-        for (auto* b : {&segcnt, &outs, &rel_off, &rel_slot, &rel_cpu, &rel_mem, &rel_gpu})
+        tlhdr.release();
+        for (auto* b : {&outs, &rel_off, &rel_slot, &rel_cpu, &rel_mem, &rel_gpu})
             b->release();
         slab.release();
         tl_err.release();
@@ -702,6 +706,13 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     int32_t maxlen = 1;
     for (int k = 0; k < C; ++k) maxlen = std::max(maxlen, c->nb[k + 1] - c->nb[k]);
     const size_t lds = commit_tl_lds_bytes(maxlen);
+    const int runs = commit_tl_runs(maxlen);
+    int slices = std::max(1, TL_SLICES / shards), tl_min_sub = TL_MIN_SUB;
+    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 512 / (KS * shards)));
+    if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
+    if (runs < 1)
+        return fail(FIT_E_INVAL, "partition component of %d nodes is too large for the timeline "
+                                 "commit's LDS", maxlen);
     float ms;
     for (;;) {
         int64_t blocks = 0, slots = 0, cand_n = 0, evals = 0;
@@ -716,7 +727,9 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
             const int32_t per = (len + shards - 1) / shards;
             P.sb = std::min(P.ne, P.nb + per * srank);
             P.se = std::min(P.ne, P.sb + per);
-            P.sub = std::max(MIN_SUB, (per + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
+            // more, shorter block-slices than the plain fit: a run walk costs more per node, so
+            // the scan wants more waves in flight; candidate entries per job stay <= 256
+            P.sub = std::max(tl_min_sub, (per + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
             P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
             epl = std::max(epl, (shards * P.nslice * KS + 63) / 64);
             P.jbase = cur[k];
@@ -742,7 +755,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
                                st));
         HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * slots, st));
         HIP_TRY(hipEventRecord(c->ev[0], st));
-        HIP_TRY(launch_scan_tl((int)blocks, st, c->rec.p, c->slab.p, c->segcnt.p, c->jl.p, cpu, mem,
+        HIP_TRY(launch_scan_tl((int)blocks, st, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem,
                                gpu, wall, part, c->plan.p, C, c->cand.p + (size_t)srank * cand_n,
                                c->bnd.p, c->wjob.p, c->tl_slots, c->tl_slot_min));
         HIP_TRY(hipEventRecord(c->ev[1], st));
@@ -752,9 +765,9 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
             if (rc) return rc;
         }
         HIP_TRY(hipEventRecord(c->ev[2], st));
-        HIP_TRY(launch_commit_tl(C, epl, lds, st, c->rec.p, c->slab.p, c->segcnt.p, c->plan.p,
-                                 c->cand.p, cand_n, shards, c->bnd.p, c->wjob.p, out, outs,
-                                 c->res.p, c->tl_slots));
+        HIP_TRY(launch_commit_tl(C, epl, lds, st, c->slab.p, c->tlhdr.p, c->plan.p, c->cand.p,
+                                 cand_n, shards, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
+                                 c->res.p, c->tl_slots, runs));
         HIP_TRY(hipEventRecord(c->ev[3], st));
         HIP_TRY(hipMemcpyAsync(c->h_res.p, c->res.p, sizeof(CommitResult) * C,
                                hipMemcpyDeviceToHost, st));
@@ -787,15 +800,15 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
 }
 
 int load_timeline_impl(fit_ctx* c, int32_t slots, int32_t slot_min, int64_t ne) {
-    if (c->segcnt.ensure(std::max(c->nn, 1)) ||
+    if (c->tlhdr.ensure(std::max(c->nn, 1)) ||
         c->slab.ensure((size_t)std::max(c->nn, 1) * TL_MAX_SLOTS) || c->tl_err.ensure(1) ||
         c->h_tl_err.ensure(1))
         return FIT_E_OOM;
     HIP_TRY(hipMemsetAsync(c->tl_err.p, 0, 4, c->st));
     HIP_TRY(launch_build_tl(c->st, c->col_cpu.p, c->col_mem.p, c->col_gpu.p, c->col_av.p,
-                            c->perm.p, c->nn, slots, slot_min, ne >= 0 ? c->rel_off.p : nullptr,
+                            c->col_mask.p, c->perm.p, c->nn, slots, slot_min, ne >= 0 ? c->rel_off.p : nullptr,
                             c->rel_slot.p, c->rel_cpu.p, c->rel_mem.p, c->rel_gpu.p, c->slab.p,
-                            c->segcnt.p, c->tl_err.p));
+                            c->tlhdr.p, c->tl_err.p));
     HIP_TRY(hipMemcpyAsync(c->h_tl_err.p, c->tl_err.p, 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     if (c->h_tl_err.p[0])
@@ -1191,7 +1204,7 @@ int fit_read_timeline(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
     int rc = 0;
     for (auto& x : d)
         if (hipMemsetAsync(x.p, 0xff, sizeof(int32_t) * cells, c->st) != hipSuccess) rc = FIT_E_HIP;
-    if (rc || launch_expand_tl(c->st, c->rec.p, c->slab.p, c->segcnt.p, c->nn, c->tl_slots, d[0].p,
+    if (rc || launch_expand_tl(c->st, c->perm.p, c->slab.p, c->tlhdr.p, c->nn, c->tl_slots, d[0].p,
                          d[1].p, d[2].p) != hipSuccess ||
         hipMemcpyAsync(cpu, d[0].p, sizeof(int32_t) * cells, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
         hipMemcpyAsync(mem, d[1].p, sizeof(int32_t) * cells, hipMemcpyDeviceToHost, c->st) != hipSuccess ||

@@ -62,6 +62,8 @@ struct CompOut {
 // ---- SPEC §2b time-windowed backfill (fit_timeline.hip) --------------------
 constexpr int TL_MAX_SLOTS = 1024;  // horizon limit (slots); the C5 horizon
 constexpr int TL_UCAP = 64;         // dirty nodes per component per round (one per lane)
+constexpr int TL_SLICES = 16;       // block-slices per job (over all ranks) in the timeline scan
+constexpr int TL_MIN_SUB = 32;      // minimum nodes per wave sub-slice in the timeline scan
 constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position
 constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;
 
@@ -69,6 +71,19 @@ constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;
 // list is canonical (adjacent runs differ) and ends at the horizon; at most TL_MAX_SLOTS runs.
 struct alignas(16) Seg {
     int32_t end, cpu, mem, gpu;
+};
+
+constexpr int TL_HEAD = 4;  // runs of each node copied into its header (the scan's common case)
+
+// Per-node header of a run list, 96 B, contiguous over nodes (the scan streams it): run count,
+// the largest free value of each column over the timeline as built (reservations only lower
+// values, so it stays an upper bound: a job whose demand exceeds it can never fit the node),
+// partition mask, and a copy of the first TL_HEAD runs.
+struct alignas(32) TlHdr {
+    int32_t cnt, cpu, mem, gpu;
+    uint32_t mask;
+    int32_t pad[3];
+    Seg head[TL_HEAD];
 };
 
 struct CommitResult {

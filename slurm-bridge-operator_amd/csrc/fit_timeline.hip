@@ -3,16 +3,43 @@
 //
 // Node state is each node's free-resource timeline, run-length encoded: a canonical list of runs
 // (Seg: end slot, cpu, mem, gpu) in a fixed per-node slab of TL_MAX_SLOTS entries in HBM (only
-// the used prefix is ever touched, so the working set is the live runs, L2/MALL resident).  The
-// speculative rounds are the same as the plain fit (fit_common.h): k_scan_tl keeps the exact
-// top-KS keys per (job, block-slice) plus a bound against the round-start timelines; k_commit_tl
-// walks the window in priority order with a dirty set of at most TL_UCAP nodes (one per lane),
-// re-evaluating dirty nodes exactly on their current runs, and reserves each decision in place.
+// the used prefix is ever touched), plus a contiguous 96-B header per node (run count, column
+// ceilings, partition mask, first TL_HEAD runs) that the scan streams.  The speculative rounds are
+// the plain fit's (fit_common.h): k_scan_tl keeps the exact top-KS keys per (job, block-slice)
+// plus a bound against the round-start timelines; k_commit_tl walks the window in priority order
+// with a dirty set of at most TL_UCAP nodes (one per lane) whose run lists (and prefix minima)
+// live in LDS, re-evaluates them exactly per job and reserves each decision in place.
 //   key = start << 54 | score << 22 | position   (earliest start, then best fit, then node)
 // The sequential semantics reproduced bit-exactly is oracle/fitref_tl.c:ref_place_tl.
+#include <algorithm>
+
 #include "fit_common.h"
 
 namespace fitgpu {
+
+constexpr int TL_PM_STEPS = 32;     // LDS run lists hold <= 2 * TL_PM_STEPS = 64 runs
+constexpr int32_t TL_BIG = 0x7fffffff;
+
+#ifdef FIT_STAMPS
+// diagnostic build only.  scan: [0] node-loop cycles (sum over waves), [1] nodes, [2] long-walk
+// batches, [3] nodes with > TL_HEAD runs, [4] waves.  commit: [comp][0..4] cycles in clean check /
+// dirty eval / new dirty / reserve / tail, [5] jobs, [6] new dirty nodes, [7] round-end cycles
+__device__ unsigned long long g_tlsc[8];
+__device__ unsigned long long g_tlst[64][12];
+#define TL_CLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define TL_ACC(i, a, b) tacc[i] += (b) - (a)
+#else
+#define TL_CLK(v)
+#define TL_ACC(i, a, b)
+#endif
+
+// a VGPR zero the compiler cannot see through: keeps wave-uniform loads on the vector path
+// (vmcnt, in order, so a load issued for the next item is not waited for with this one's)
+__device__ __forceinline__ int tl_vzero() {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
 
 __device__ __forceinline__ uint64_t tl_key(int32_t s, int32_t mc, int32_t mm, int32_t mg,
                                            int32_t jc, int32_t jm, int32_t jg, uint32_t pos) {
@@ -22,59 +49,71 @@ __device__ __forceinline__ uint64_t tl_key(int32_t s, int32_t mc, int32_t mm, in
     return ((uint64_t)(uint32_t)s << 54) | ((uint64_t)sc << TL_POS_BITS) | pos;
 }
 
-// Earliest start of a d-slot window whose every run holds (jc, jm, jg), and its key.  One lane
-// per (job, node); `live` lanes walk the node's runs [0, cnt).  A lane stops early once every
-// start it could still find is later than `cut`'s start (its key would lose to `cut`).  The loop
-// is wave-uniform (ballot exit), so with a uniform `sg` the run loads are scalar.
+// Per-lane state of the earliest-start walk over one node's runs.
+struct TlWalk {
+    int32_t ra, mc, mm, mg, a;  // start of the current feasible stretch (-1: none), its minima, run start
+    uint64_t key;
+    bool live;
+};
+
+// One run: extend / break the feasible stretch; a stretch of d slots gives the key.  A lane
+// stops once every start it could still find is later than `lim` (the start of its cut key).
+__device__ __forceinline__ void tl_step(TlWalk& w, int32_t end, int32_t c, int32_t m, int32_t g,
+                                        int32_t jc, int32_t jm, int32_t jg, int32_t d, int32_t H,
+                                        int32_t lim, uint32_t pos) {
+    if (!w.live) return;
+    if (c >= jc && m >= jm && g >= jg) {
+        if (w.ra < 0) {
+            w.ra = w.a;
+            w.mc = c;
+            w.mm = m;
+            w.mg = g;
+        } else {
+            w.mc = min(w.mc, c);
+            w.mm = min(w.mm, m);
+            w.mg = min(w.mg, g);
+        }
+        if (end - w.ra >= d) {
+            w.key = tl_key(w.ra, w.mc, w.mm, w.mg, jc, jm, jg, pos);
+            w.live = false;
+        } else if (w.ra > lim) {
+            w.live = false;
+        }
+    } else {
+        w.ra = -1;
+        if (end + d > H || end > lim) w.live = false;  // no (competitive) start left
+    }
+    w.a = end;
+}
+
+// Earliest start of a d-slot window whose every run holds (jc, jm, jg), and its key, for `live`
+// lanes walking their node's runs [0, cnt) (any address space; the loop is wave-uniform).
 __device__ __forceinline__ uint64_t tl_eval(const Seg* sg, int cnt, bool live, int32_t jc,
                                             int32_t jm, int32_t jg, int32_t d, int32_t H,
                                             uint32_t pos, uint64_t cut) {
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
-    uint64_t key = KEY_INF;
-    int32_t ra = -1, mc = 0, mm = 0, mg = 0, a = 0;
-    live = live && d <= H;
+    TlWalk w{-1, 0, 0, 0, 0, KEY_INF, live && d <= H};
     for (int i = 0;; ++i) {
-        const bool l = live && i < cnt;
-        if (!__ballot(l)) break;
-        if (l) {
+        if (!__ballot(w.live && i < cnt)) break;
+        if (w.live && i < cnt) {
             const Seg g = sg[i];
-            if (g.cpu >= jc && g.mem >= jm && g.gpu >= jg) {
-                if (ra < 0) {
-                    ra = a;
-                    mc = g.cpu;
-                    mm = g.mem;
-                    mg = g.gpu;
-                } else {
-                    mc = min(mc, g.cpu);
-                    mm = min(mm, g.mem);
-                    mg = min(mg, g.gpu);
-                }
-                if (g.end - ra >= d) {
-                    key = tl_key(ra, mc, mm, mg, jc, jm, jg, pos);
-                    live = false;
-                } else if (ra > lim) {
-                    live = false;
-                }
-            } else {
-                ra = -1;
-                if (g.end + d > H || g.end > lim) live = false;  // no (competitive) start left
-            }
-            a = g.end;
+            tl_step(w, g.end, g.cpu, g.mem, g.gpu, jc, jm, jg, d, H, lim, pos);
         }
     }
-    return key;
+    return w.key;
 }
 
 // ------------------------------------------------------------------------------ k_build_tl
-// One thread per node position: base free columns + sorted release events → canonical runs.
-// Values are clamped to [-1, INT32_MAX]; slots >= min(H, avail / slot_min) hold -1.
+// One thread per node position: base free columns + sorted release events → canonical runs and
+// the node header.  Values are clamped to [-1, INT32_MAX]; slots >= min(H,
+// avail / slot_min) hold -1.
 __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __restrict__ mem,
                            const int32_t* __restrict__ gpu, const int32_t* __restrict__ av,
-                           const int32_t* __restrict__ perm, int32_t nn, int32_t H,
-                           int32_t slot_min, const int32_t* __restrict__ off,
+                           const uint32_t* __restrict__ mask, const int32_t* __restrict__ perm,
+                           int32_t nn, int32_t H, int32_t slot_min, const int32_t* __restrict__ off,
                            const int32_t* __restrict__ rs, const int32_t* __restrict__ rc,
                            const int32_t* __restrict__ rm, const int32_t* __restrict__ rg,
-                           Seg* __restrict__ slab, int32_t* __restrict__ segcnt,
+                           Seg* __restrict__ slab, TlHdr* __restrict__ hdr,
                            uint32_t* __restrict__ err) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nn) return;
@@ -82,7 +121,7 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
     Seg* sg = slab + (int64_t)i * TL_MAX_SLOTS;
     const int32_t u = av[x] < 0 ? 0 : min(av[x] / slot_min, H);
     int64_t ac = cpu[x], am = mem[x], ag = gpu[x];
-    auto cl = [](int64_t v) { return (int32_t)max<int64_t>(-1, min<int64_t>(v, 0x7fffffff)); };
+    auto cl = [](int64_t v) { return (int32_t)max<int64_t>(-1, min<int64_t>(v, TL_BIG)); };
     int n = 0, a = 0;
     auto emit = [&](int32_t end, int32_t vc, int32_t vm, int32_t vg) {
         if (end <= a) return;
@@ -114,21 +153,65 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
     }
     emit(u, cl(ac), cl(am), cl(ag));
     emit(H, -1, -1, -1);
-    segcnt[i] = n;
+    TlHdr h;
+    h.cnt = n;
+    h.cpu = h.mem = h.gpu = -1;
+    for (int k = 0; k < n; ++k) {
+        h.cpu = max(h.cpu, sg[k].cpu);
+        h.mem = max(h.mem, sg[k].mem);
+        h.gpu = max(h.gpu, sg[k].gpu);
+    }
+    h.mask = mask[x];
+    h.pad[0] = h.pad[1] = h.pad[2] = 0;
+    for (int k = 0; k < TL_HEAD; ++k) h.head[k] = k < n ? sg[k] : Seg{H, -1, -1, -1};
+    hdr[i] = h;
 }
 
 // ----------------------------------------------------------------------------- k_scan_tl
-// Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices; each wave walks
-// its nodes' runs with wave-uniform (scalar) loads and keeps the exact top-KS keys per lane;
-// the 8 lists merge through LDS exactly as in k_scan (fit_common.h).
+// Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices; each wave walks its
+// nodes in order.  Node headers (96 B, contiguous) stream in through two register sets with
+// vector loads two nodes ahead (in-order vmcnt, so the wait for node x never waits for x+1);
+// the rare walk past the header's runs reads the slab with scalar loads.  Top-KS lists, bound
+// and the LDS merge tree are k_scan's (fit_common.h).
+__device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec& J, int32_t H,
+                                             const Seg* __restrict__ slab, uint64_t (&key)[KS],
+                                             unsigned long long& batches) {
+    const uint64_t cut = key[KS - 1];
+    const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
+    TlWalk w{-1, 0, 0, 0, 0, KEY_INF,
+             (h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu && J.mem <= h.mem &&
+                 J.gpu <= h.gpu};
+    const int cn = __builtin_amdgcn_readfirstlane(h.cnt);
+#pragma unroll
+    for (int i = 0; i < TL_HEAD; ++i)
+        if (i < cn)
+            tl_step(w, h.head[i].end, h.head[i].cpu, h.head[i].mem, h.head[i].gpu, J.cpu, J.mem,
+                    J.gpu, J.wall, H, lim, (uint32_t)x);
+    if (cn > TL_HEAD) {
+        const Seg* sg = slab + (int64_t)x * TL_MAX_SLOTS;
+        for (int b = TL_HEAD; b < cn; b += TL_HEAD) {
+            if (!__ballot(w.live)) break;
+            ++batches;
+            Seg r4[TL_HEAD];
+#pragma unroll
+            for (int i = 0; i < TL_HEAD; ++i) r4[i] = sg[b + i];  // inside the slab (TL_HEAD | 1024)
+#pragma unroll
+            for (int i = 0; i < TL_HEAD; ++i)
+                if (b + i < cn)
+                    tl_step(w, r4[i].end, r4[i].cpu, r4[i].mem, r4[i].gpu, J.cpu, J.mem, J.gpu,
+                            J.wall, H, lim, (uint32_t)x);
+        }
+    }
+    if (w.key < key[KS - 1]) topk_insert(key, w.key);
+}
+
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
-    const NodeRec* __restrict__ rec, const Seg* __restrict__ slab,
-    const int32_t* __restrict__ segcnt, const int32_t* __restrict__ jl,
-    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
-    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
-    const uint16_t* __restrict__ jpart, const CompPlan* __restrict__ plan, int ncomp,
-    uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob,
-    int32_t H, int32_t slot_min) {
+    const Seg* __restrict__ slab, const TlHdr* __restrict__ hdr,
+    const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
+    const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
+    const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
+    const CompPlan* __restrict__ plan, int ncomp, uint64_t* __restrict__ cand,
+    uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob, int32_t H, int32_t slot_min) {
     __shared__ uint64_t xk[SCAN_WAVES / 2][KS][64];
     const int c = find_comp(plan, ncomp, blockIdx.x);
     const CompPlan P = plan[c];
@@ -148,7 +231,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
     J.gpu = active ? jgpu[J.q] : 0;
     // wall → slots occupied: ceil(wall / slot_min), at least 1 (oracle ref_slots)
     const int64_t dw = active ? ((int64_t)jwall[J.q] + slot_min - 1) / slot_min : 1;
-    J.wall = (int32_t)max<int64_t>(1, min<int64_t>(dw, 0x7fffffff));
+    J.wall = (int32_t)max<int64_t>(1, min<int64_t>(dw, TL_BIG));
     J.pbit = active ? (1u << jpart[J.q]) : 0u;
     J.k = 1;
     J.pad = 0;
@@ -158,13 +241,36 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
     for (int i = 0; i < KS; ++i) key[i] = KEY_INF;
     const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
     const int n1 = min(P.se, n0 + P.sub);
-    for (int x = n0; x < n1; ++x) {
-        const NodeRec r = rec[x];
-        const bool live = (r.mask & J.pbit) != 0u;
-        const uint64_t k = tl_eval(slab + (int64_t)x * TL_MAX_SLOTS, segcnt[x], live, J.cpu,
-                                   J.mem, J.gpu, J.wall, H, (uint32_t)x, key[KS - 1]);
-        if (k < key[KS - 1]) topk_insert(key, k);
+    unsigned long long batches = 0, longn = 0;
+#ifdef FIT_STAMPS
+    const unsigned long long sc_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (n0 < n1) {
+        const int z = tl_vzero();
+        TlHdr h0 = hdr[n0 + z], h1 = hdr[min(n0 + 1, n1 - 1) + z];
+        for (int x = n0; x < n1; x += 2) {
+            longn += h0.cnt > TL_HEAD;
+            tl_scan_node(h0, x, J, H, slab, key, batches);
+            h0 = hdr[min(x + 2, n1 - 1) + z];
+            if (x + 1 < n1) {
+                longn += h1.cnt > TL_HEAD;
+                tl_scan_node(h1, x + 1, J, H, slab, key, batches);
+                h1 = hdr[min(x + 3, n1 - 1) + z];
+            }
+        }
     }
+#ifdef FIT_STAMPS
+    if (lane == 0) {
+        atomicAdd(&g_tlsc[0], __builtin_amdgcn_s_memtime() - sc_t0);
+        atomicAdd(&g_tlsc[1], (unsigned long long)max(n1 - n0, 0));
+        atomicAdd(&g_tlsc[2], batches);
+        atomicAdd(&g_tlsc[3], longn);
+        atomicAdd(&g_tlsc[4], 1ull);
+    }
+#else
+    (void)batches;
+    (void)longn;
+#endif
 #pragma unroll
     for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
         if (wave >= h && wave < 2 * h) {
@@ -200,14 +306,34 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-// Reserve (jc, jm, jg) on slots [s, e) of one node's run list, by the whole wave: the runs from
-// the one before the window to the end are split at s and e into LDS scratch (pass 1, prefix
-// sums over piece counts), then equal neighbours merge and the list is written back (pass 2).
-// Only the two window edges can create runs or merge, so the list stays canonical.
-__device__ void tl_reserve(Seg* sg, int32_t* cntp, int32_t s, int32_t e, int32_t jc, int32_t jm,
-                           int32_t jg, Seg* scr) {
+// Inclusive prefix minimum over the 64 lanes (DPP: row shifts, then row broadcasts).
+__device__ __forceinline__ int32_t wave_scan_min(int32_t v) {
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
+// Prefix minima of an LDS run list (<= 64 runs): PM[i] = min over runs [0, i] per column.
+// With them, "fits from slot 0 for d slots" and that window's minimum are one search over the
+// run ends — the dirty-node fast path.
+__device__ __forceinline__ void tl_pm_build(const Seg* L, int4* PM, int n) {
     const int lane = threadIdx.x & 63;
-    const int n = __builtin_amdgcn_readfirstlane(*cntp);
+    const Seg g = lane < n ? L[lane] : Seg{0, TL_BIG, TL_BIG, TL_BIG};
+    const int32_t vc = wave_scan_min(g.cpu), vm = wave_scan_min(g.mem), vg = wave_scan_min(g.gpu);
+    if (lane < n) PM[lane] = make_int4(vc, vm, vg, 0);
+}
+
+// Reserve (jc, jm, jg) on slots [s, e) of a run list, general form (any length, any address
+// space), by the whole wave: the runs from the one before the window to the end are split at s
+// and e into LDS scratch (prefix sums over piece counts), equal neighbours merge, and the result
+// is written back.  Returns the new run count.
+__device__ __forceinline__ int tl_reserve_any(Seg* sg, int n, int32_t s, int32_t e, int32_t jc,
+                                              int32_t jm, int32_t jg, Seg* scr) {
+    const int lane = threadIdx.x & 63;
     int i0 = n;
     for (int b = 0; b < n; b += 64) {
         const int i = b + lane;
@@ -244,30 +370,78 @@ __device__ void tl_reserve(Seg* sg, int32_t* cntp, int32_t s, int32_t e, int32_t
     int no = 0;
     for (int b = 0; b < np; b += 64) {
         const int k = b + lane;
-        const bool v = k < np;
-        const Seg p = v ? scr[k] : Seg{0, 0, 0, 0};
+        const Seg p = k < np ? scr[k] : Seg{0, 0, 0, 0};
         const Seg q = k + 1 < np ? scr[k + 1] : Seg{0, -2, -2, -2};
-        const bool keep = v && (k + 1 >= np || p.cpu != q.cpu || p.mem != q.mem || p.gpu != q.gpu);
+        const bool keep = k < np && (k + 1 >= np || p.cpu != q.cpu || p.mem != q.mem || p.gpu != q.gpu);
         const uint64_t mk = __ballot(keep);
         if (keep) sg[r0 + no + lanes_below(mk)] = p;
         no += __popcll(mk);
     }
-    if (lane == 0) *cntp = r0 + no;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // later reads of this list see the writes
+    return r0 + no;
 }
 
-// One wave per component: the speculative-prefix commit of the plain fit (fit_common.h) with
-// run-list evaluation of the dirty nodes (one per lane) and in-place reservation.
+// Reserve on an LDS list of n <= 64 runs held in registers: one read, the edges resolved with
+// readlanes, one write of the shifted runs.  Runs overlapping [s, e) lose the demand; the run
+// holding s (e) splits when s (e) falls inside it; the first (last) reduced run merges into its
+// left (right) neighbour when their values become equal — the only places the list can change
+// shape, so it stays canonical.  Returns the new count, or -1 (list untouched) if it would
+// exceed `cap` runs.
+__device__ __forceinline__ int tl_reserve_lds(Seg* L, int n, int cap, int32_t s, int32_t e,
+                                              int32_t jc, int32_t jm, int32_t jg) {
+    const int lane = threadIdx.x & 63;
+    const bool v = lane < n;
+    const Seg g = v ? L[lane] : Seg{TL_BIG, 0, 0, 0};
+    const int32_t a = (v && lane > 0) ? L[lane - 1].end : 0;
+    const uint64_t mov = __ballot(v && a < e && g.end > s);
+    const int i0 = __builtin_ctzll(mov), i1 = 63 - __builtin_clzll(mov);
+    const int32_t a0 = __builtin_amdgcn_readlane(a, i0), e1 = __builtin_amdgcn_readlane(g.end, i1);
+    const int head = a0 < s, tail = e1 > e;
+    const int32_t c0 = __builtin_amdgcn_readlane(g.cpu, i0) - jc;
+    const int32_t m0 = __builtin_amdgcn_readlane(g.mem, i0) - jm;
+    const int32_t g0 = __builtin_amdgcn_readlane(g.gpu, i0) - jg;
+    const int32_t c1 = __builtin_amdgcn_readlane(g.cpu, i1) - jc;
+    const int32_t m1 = __builtin_amdgcn_readlane(g.mem, i1) - jm;
+    const int32_t g1 = __builtin_amdgcn_readlane(g.gpu, i1) - jg;
+    const int il = max(i0 - 1, 0), ir = min(i1 + 1, 63);
+    const int mergeL = !head && i0 > 0 && __builtin_amdgcn_readlane(g.cpu, il) == c0 &&
+                       __builtin_amdgcn_readlane(g.mem, il) == m0 &&
+                       __builtin_amdgcn_readlane(g.gpu, il) == g0;
+    const int mergeR = !tail && i1 < n - 1 && __builtin_amdgcn_readlane(g.cpu, ir) == c1 &&
+                       __builtin_amdgcn_readlane(g.mem, ir) == m1 &&
+                       __builtin_amdgcn_readlane(g.gpu, ir) == g1;
+    const int nn = n + head + tail - mergeL - mergeR;
+    if (nn > cap) return -1;
+    const int sh = head - mergeL;                       // index shift of the reduced runs
+    const int st = head + tail - mergeL - mergeR;       // index shift of the runs after them
+    if (v && lane >= i0 && lane <= i1) {
+        if (lane == i0 && head) L[i0] = Seg{s, g.cpu, g.mem, g.gpu};
+        if (!(lane == i1 && mergeR))
+            L[lane + sh] = Seg{min(g.end, e), g.cpu - jc, g.mem - jm, g.gpu - jg};
+        if (lane == i1 && tail) L[i1 + sh + 1] = g;
+    } else if (v && lane > i1 && st != 0) {
+        L[lane + st] = g;
+    }
+    return nn;
+}
+
+// One wave per component: the speculative-prefix commit (fit_common.h) over timelines.  A node
+// that becomes dirty has its run list copied into an LDS region of R (<= 64) runs with prefix
+// minima (lists that are or grow longer move to the global slab and take the general paths).
+// Per job, on the fast path, every wait is on LDS or on loads issued one job earlier: the job
+// stream (row, bound, candidate keys) is prefetched with vector loads (in-order vmcnt), and the
+// dirty evaluation, reservation and prefix-minimum update are LDS-only.
 template <int EPL>
 __global__ __launch_bounds__(64) void k_commit_tl(
-    const NodeRec* __restrict__ rec, Seg* __restrict__ slab, int32_t* __restrict__ segcnt,
-    const CompPlan* __restrict__ plan, const uint64_t* __restrict__ cand, int64_t rank_stride,
-    int nranks, const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
-    int32_t* __restrict__ out, int32_t* __restrict__ outs, CommitResult* __restrict__ res,
-    int32_t H) {
+    Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const CompPlan* __restrict__ plan,
+    const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
+    const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
+    const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
+    CommitResult* __restrict__ res, int32_t H, int32_t R) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Seg* scr = reinterpret_cast<Seg*>(smem);
-    uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem + sizeof(Seg) * TL_MAX_SLOTS);
+    Seg* scr = reinterpret_cast<Seg*>(smem);                // general-path scratch
+    Seg* lr = scr + TL_MAX_SLOTS;                           // TL_UCAP regions of R runs
+    int4* pmr = reinterpret_cast<int4*>(lr + TL_UCAP * R);  // their prefix minima
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(pmr + TL_UCAP * R);
     const int c = blockIdx.x;
     const CompPlan P = plan[c];
     const int lane = threadIdx.x & 63;
@@ -290,70 +464,211 @@ __global__ __launch_bounds__(64) void k_commit_tl(
         off[k] = has[k] ? g * rank_stride + P.cand_off + (e - g * per_rank) : P.cand_off;
     }
     const uint32_t nb = (uint32_t)P.nb;
+    const int z = tl_vzero();
     int nu = 0, placed = 0, stop = 0, t = 0;
-    uint32_t upos = 0u, umask = 0u;  // dirty node of this lane (lane < nu)
+    // this lane's dirty node (lane < nu): position, mask, id, run count, column ceilings, and
+    // whether its list lives in the global slab instead of LDS
+    uint32_t upos = 0u, umask = 0u;
+    int32_t uorig = -1, ucnt = 0, ucc = -1, ucm = -1, ucg = -1;
+    bool uglob = false;
+    const Seg* const mine = lr + lane * R;
+    const int4* const pmine = pmr + lane * R;
+#ifdef FIT_STAMPS
+    unsigned long long tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    JobRec J = wjob[P.slot0 + z];
+    uint64_t B = bnd[P.slot0 + z];
+    uint64_t kr[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) kr[k] = cand[off[k]];
     for (; t < P.w; ++t) {
-        const JobRec J = wjob[P.slot0 + t];
-        const uint64_t B = bnd[P.slot0 + t];
+        TL_CLK(c0);
         uint64_t cm = KEY_INF;
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
-            const uint64_t kk = cand[off[k] + (int64_t)t * per_rank];
+            const uint64_t kk = kr[k];
             const bool v = has[k] && kk <= B && kk != KEY_INF;
             const uint32_t rel = v ? ((uint32_t)kk & TL_POS_MASK) - nb : 0u;
             const bool clean = v && !((bitmap[rel >> 5] >> (rel & 31)) & 1u);
             cm = umin64(cm, clean ? kk : KEY_INF);
         }
+        const int32_t jq = __builtin_amdgcn_readfirstlane(J.q);
+        const int32_t jc = __builtin_amdgcn_readfirstlane(J.cpu);
+        const int32_t jm = __builtin_amdgcn_readfirstlane(J.mem);
+        const int32_t jg = __builtin_amdgcn_readfirstlane(J.gpu);
+        const int32_t jd = __builtin_amdgcn_readfirstlane(J.wall);
+        const uint32_t jp = (uint32_t)__builtin_amdgcn_readfirstlane((int)J.pbit);
+        const uint64_t Bc =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(B >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)B);
+        {  // the next job's stream, in flight during this one
+            const int tn = min(t + 1, P.w - 1);
+            J = wjob[P.slot0 + tn + z];
+            B = bnd[P.slot0 + tn + z];
+#pragma unroll
+            for (int k = 0; k < EPL; ++k) kr[k] = cand[off[k] + (int64_t)tn * per_rank];
+        }
         const uint64_t cw = wave_min_key(cm);
-        const bool dl = lane < nu && (umask & J.pbit) != 0u;
-        const uint64_t dk = tl_eval(slab + (int64_t)upos * TL_MAX_SLOTS, dl ? segcnt[upos] : 0, dl,
-                                    J.cpu, J.mem, J.gpu, J.wall, H, upos, cw);
+        TL_CLK(c1);
+        TL_ACC(0, c0, c1);
+        const bool dl = lane < nu && (umask & jp) != 0u && jc <= ucc && jm <= ucm && jg <= ucg &&
+                        jd <= H;
+        // LDS lists: a start at slot 0 through the prefix minima — k = the first run ending at or
+        // after d, by a 4-ary search (three rounds of three independent reads); a later start
+        // (only when it can still win) or a global list walks the runs
+        uint64_t dk = KEY_INF;
+        bool walk = dl && uglob;
+        if (dl && !uglob) {
+            int k = 0;
+#pragma unroll
+            for (int q = 16; q >= 1; q >>= 2) {
+                const int i1 = k + q - 1, i2 = k + 2 * q - 1, i3 = k + 3 * q - 1;
+                const int32_t x1 = i1 < ucnt ? mine[i1].end : TL_BIG;
+                const int32_t x2 = i2 < ucnt ? mine[i2].end : TL_BIG;
+                const int32_t x3 = i3 < ucnt ? mine[i3].end : TL_BIG;
+                k += q * ((x1 < jd) + (x2 < jd) + (x3 < jd));
+            }
+            const int4 pk = pmine[k];
+            if (pk.x >= jc && pk.y >= jm && pk.z >= jg)
+                dk = tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, upos);
+            else
+                walk = cw == KEY_INF || (cw >> 54) > 0;
+        }
+        TL_CLK(c1b);
+        TL_ACC(8, c1, c1b);
+        if (__ballot(walk)) {
+#ifdef FIT_STAMPS
+            tacc[10] += 1;
+#endif
+            const uint64_t wl = tl_eval(mine, ucnt, walk && !uglob, jc, jm, jg, jd, H, upos, cw);
+            const uint64_t wg = tl_eval(slab + (int64_t)upos * TL_MAX_SLOTS, ucnt, walk && uglob,
+                                        jc, jm, jg, jd, H, upos, cw);
+            dk = walk ? (uglob ? wg : wl) : dk;
+        }
+        TL_CLK(c1c);
+        TL_ACC(9, c1b, c1c);
         const uint64_t best = umin64(cw, wave_min_key(dk));
-        if (B != KEY_INF && best > B) {
+        TL_CLK(c2);
+        TL_ACC(1, c1, c2);
+        if (Bc != KEY_INF && best > Bc) {
             stop = 1;  // a node outside the candidate lists could win: rescan next round
             break;
         }
         int32_t node = -1, start = -1;
         if (best != KEY_INF) {
             const uint32_t pos = (uint32_t)best & TL_POS_MASK;
-            if (__ballot(dk == best) == 0ull) {  // a clean candidate wins: it becomes dirty
+            const uint64_t dm = __ballot(dk == best);
+            TL_CLK(c3);
+            int l;
+            if (dm == 0ull) {  // a clean candidate wins: it becomes dirty lane nu
                 if (nu == TL_UCAP) {
                     stop = 2;
                     break;
                 }
-                if (lane == nu) {
+                l = nu++;
+                const TlHdr h0 = hdr[pos + z];
+                const int n0 = __builtin_amdgcn_readfirstlane(h0.cnt);
+                const bool g = n0 > R;
+                if (!g) {
+                    const Seg* src = slab + (int64_t)pos * TL_MAX_SLOTS;
+                    Seg* dst = lr + l * R;
+                    if (lane < n0) dst[lane] = src[lane];  // n0 <= R <= 64
+                    tl_pm_build(dst, pmr + l * R, n0);
+                }
+                if (lane == l) {
                     upos = pos;
-                    umask = rec[pos].mask;
+                    umask = h0.mask;
+                    uorig = perm[pos];
+                    ucnt = n0;
+                    ucc = h0.cpu;
+                    ucm = h0.mem;
+                    ucg = h0.gpu;
+                    uglob = g;
                 }
                 if (lane == 0) {
                     const uint32_t rel = pos - nb;
                     bitmap[rel >> 5] |= 1u << (rel & 31);
                 }
-                ++nu;
+#ifdef FIT_STAMPS
+                tacc[6] += 1;
+#endif
+            } else {
+                l = __builtin_ctzll(dm);
             }
+            TL_CLK(c4);
+            TL_ACC(2, c3, c4);
+            const bool g = __builtin_amdgcn_readlane((int)uglob, l) != 0;
+            const int n = __builtin_amdgcn_readlane(ucnt, l);
             start = (int32_t)(best >> 54);
-            tl_reserve(slab + (int64_t)pos * TL_MAX_SLOTS, segcnt + pos, start, start + J.wall,
-                       J.cpu, J.mem, J.gpu, scr);
-            node = rec[pos].orig;
+            int nn;
+            if (!g) {
+                Seg* L = lr + l * R;
+                nn = tl_reserve_lds(L, n, R, start, start + jd, jc, jm, jg);
+                if (nn >= 0) {
+                    tl_pm_build(L, pmr + l * R, nn);
+                } else {  // outgrows its LDS region: move the list to the global slab
+                    Seg* gl = slab + (int64_t)pos * TL_MAX_SLOTS;
+                    if (lane < n) gl[lane] = L[lane];
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    nn = tl_reserve_any(gl, n, start, start + jd, jc, jm, jg, scr);
+                    if (lane == l) uglob = true;
+                }
+            } else {
+                nn = tl_reserve_any(slab + (int64_t)pos * TL_MAX_SLOTS, n, start, start + jd, jc,
+                                    jm, jg, scr);
+            }
+            if (lane == l) ucnt = nn;
+            node = __builtin_amdgcn_readlane(uorig, l);
             ++placed;
+            TL_CLK(c5);
+            TL_ACC(3, c4, c5);
         }
+        TL_CLK(c6);
         if (lane == 0) {
-            out[J.q] = node;
-            outs[J.q] = start;
+            out[jq] = node;
+            outs[jq] = start;
         }
+        TL_CLK(c7);
+        TL_ACC(4, c6, c7);
     }
+    TL_CLK(e0);
+    // round end: LDS lists back to their slabs (the next scan reads them), headers for all
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // global-list writes before re-reads
+    for (int l = 0; l < nu; ++l) {
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)upos, l);
+        const int n = __builtin_amdgcn_readlane(ucnt, l);
+        Seg* dst = slab + (int64_t)p * TL_MAX_SLOTS;
+        Seg hd = Seg{H, -1, -1, -1};
+        if (!__builtin_amdgcn_readlane((int)uglob, l)) {
+            const Seg* src = lr + l * R;
+            if (lane < n) {
+                hd = src[lane];
+                dst[lane] = hd;
+            }
+        } else if (lane < TL_HEAD && lane < n) {
+            hd = dst[lane];
+        }
+        if (lane < TL_HEAD) hdr[p].head[lane] = hd;
+    }
+    if (lane < nu) hdr[upos].cnt = ucnt;
     if (lane == 0) res[c] = CommitResult{t, stop, nu, placed};
+#ifdef FIT_STAMPS
+    TL_CLK(e1);
+    tacc[7] += e1 - e0;
+    tacc[5] += t;
+    if (lane == 0)
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_tlst[c & 63][i], tacc[i]);
+#endif
 }
 
 // Dense read-back (tests, fit_read_timeline): one block per node position, threads over slots.
-__global__ void k_expand_tl(const NodeRec* __restrict__ rec, const Seg* __restrict__ slab,
-                            const int32_t* __restrict__ segcnt, int32_t H,
-                            int32_t* __restrict__ oc, int32_t* __restrict__ om,
-                            int32_t* __restrict__ og) {
+__global__ void k_expand_tl(const int32_t* __restrict__ perm, const Seg* __restrict__ slab,
+                            const TlHdr* __restrict__ hdr, int32_t H, int32_t* __restrict__ oc,
+                            int32_t* __restrict__ om, int32_t* __restrict__ og) {
     const int i = blockIdx.x;
     const Seg* sg = slab + (int64_t)i * TL_MAX_SLOTS;
-    const int n = segcnt[i];
-    const int64_t base = (int64_t)rec[i].orig * H;
+    const int n = hdr[i].cnt;
+    const int64_t base = (int64_t)perm[i] * H;
     for (int t = threadIdx.x; t < H; t += blockDim.x) {
         int lo = 0, hi = n - 1;  // first run with end > t
         while (lo < hi) {
@@ -368,41 +683,66 @@ __global__ void k_expand_tl(const NodeRec* __restrict__ rec, const Seg* __restri
     }
 }
 
+#ifdef FIT_STAMPS
+extern "C" int fit_debug_tl_stamps(unsigned long long* out /* 64 x 12 + 8 */, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tlst), sizeof(g_tlst)) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out + 64 * 12, HIP_SYMBOL(g_tlsc), sizeof(g_tlsc)) != hipSuccess) return -2;
+    if (reset) {
+        static unsigned long long zero[64][12];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tlst), zero, sizeof(zero)) != hipSuccess) return -2;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tlsc), zero, sizeof(g_tlsc)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
 // ------------------------------------------------------------------ host launch wrappers
 hipError_t launch_build_tl(hipStream_t st, const int32_t* cpu, const int32_t* mem,
-                           const int32_t* gpu, const int32_t* av, const int32_t* perm,
-                           int32_t nn, int32_t H, int32_t slot_min, const int32_t* off,
-                           const int32_t* rs, const int32_t* rc, const int32_t* rm,
-                           const int32_t* rg, Seg* slab, int32_t* segcnt, uint32_t* err) {
+                           const int32_t* gpu, const int32_t* av, const uint32_t* mask,
+                           const int32_t* perm, int32_t nn, int32_t H, int32_t slot_min,
+                           const int32_t* off, const int32_t* rs, const int32_t* rc,
+                           const int32_t* rm, const int32_t* rg, Seg* slab, TlHdr* hdr,
+                           uint32_t* err) {
     if (nn == 0) return hipSuccess;
     hipLaunchKernelGGL(k_build_tl, dim3((nn + 255) / 256), dim3(256), 0, st, cpu, mem, gpu, av,
-                       perm, nn, H, slot_min, off, rs, rc, rm, rg, slab, segcnt, err);
+                       mask, perm, nn, H, slot_min, off, rs, rc, rm, rg, slab, hdr, err);
     return hipGetLastError();
 }
 
-hipError_t launch_scan_tl(int blocks, hipStream_t st, const NodeRec* rec, const Seg* slab,
-                          const int32_t* segcnt, const int32_t* jl, const int32_t* jcpu,
-                          const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
-                          const uint16_t* jpart, const CompPlan* plan, int ncomp, uint64_t* cand,
-                          uint64_t* bnd, JobRec* wjob, int32_t H, int32_t slot_min) {
-    hipLaunchKernelGGL(k_scan_tl, dim3(blocks), dim3(SCAN_WAVES * 64), 0, st, rec, slab, segcnt,
-                       jl, jcpu, jmem, jgpu, jwall, jpart, plan, ncomp, cand, bnd, wjob, H,
-                       slot_min);
+hipError_t launch_scan_tl(int blocks, hipStream_t st, const Seg* slab, const TlHdr* hdr,
+                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
+                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                          const CompPlan* plan, int ncomp, uint64_t* cand, uint64_t* bnd,
+                          JobRec* wjob, int32_t H, int32_t slot_min) {
+    hipLaunchKernelGGL(k_scan_tl, dim3(blocks), dim3(SCAN_WAVES * 64), 0, st, slab, hdr, jl, jcpu,
+                       jmem, jgpu, jwall, jpart, plan, ncomp, cand, bnd, wjob, H, slot_min);
     return hipGetLastError();
+}
+
+// LDS of k_commit_tl: general-path scratch + TL_UCAP dirty-list regions of R runs with their
+// prefix minima + the dirty bitmap.  R is as large as 160 KiB allows, at most 64 runs.
+constexpr size_t TL_LDS_LIMIT = 160 * 1024;
+int commit_tl_runs(int32_t max_component_nodes) {
+    const size_t fixed = sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
+    if (fixed >= TL_LDS_LIMIT) return 0;
+    return (int)std::min<size_t>(2 * TL_PM_STEPS,
+                                 (TL_LDS_LIMIT - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP));
 }
 
 size_t commit_tl_lds_bytes(int32_t max_component_nodes) {
-    return sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
+    return sizeof(Seg) * TL_MAX_SLOTS +
+           (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * commit_tl_runs(max_component_nodes) +
+           (size_t)((max_component_nodes + 31) / 32) * 4;
 }
 
-hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, const NodeRec* rec,
-                            Seg* slab, int32_t* segcnt, const CompPlan* plan,
-                            const uint64_t* cand, int64_t rank_stride, int nranks,
-                            const uint64_t* bnd, const JobRec* wjob, int32_t* out, int32_t* outs,
-                            CommitResult* res, int32_t H) {
+hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg* slab,
+                            TlHdr* hdr, const CompPlan* plan, const uint64_t* cand,
+                            int64_t rank_stride, int nranks, const uint64_t* bnd,
+                            const JobRec* wjob, const int32_t* perm, int32_t* out, int32_t* outs,
+                            CommitResult* res, int32_t H, int32_t R) {
 #define FIT_COMMIT_TL(EPL)                                                                    \
-    hipLaunchKernelGGL(k_commit_tl<EPL>, dim3(ncomp), dim3(64), lds, st, rec, slab, segcnt,   \
-                       plan, cand, rank_stride, nranks, bnd, wjob, out, outs, res, H)
+    hipLaunchKernelGGL(k_commit_tl<EPL>, dim3(ncomp), dim3(64), lds, st, slab, hdr, plan,     \
+                       cand, rank_stride, nranks, bnd, wjob, perm, out, outs, res, H, R)
     if (epl <= 1) FIT_COMMIT_TL(1);
     else if (epl <= 2) FIT_COMMIT_TL(2);
     else if (epl <= 4) FIT_COMMIT_TL(4);
@@ -412,11 +752,11 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, cons
     return hipGetLastError();
 }
 
-hipError_t launch_expand_tl(hipStream_t st, const NodeRec* rec, const Seg* slab,
-                            const int32_t* segcnt, int32_t nn, int32_t H, int32_t* oc,
-                            int32_t* om, int32_t* og) {
+hipError_t launch_expand_tl(hipStream_t st, const int32_t* perm, const Seg* slab,
+                            const TlHdr* hdr, int32_t nn, int32_t H, int32_t* oc, int32_t* om,
+                            int32_t* og) {
     if (nn == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_expand_tl, dim3(nn), dim3(256), 0, st, rec, slab, segcnt, H, oc, om, og);
+    hipLaunchKernelGGL(k_expand_tl, dim3(nn), dim3(256), 0, st, perm, slab, hdr, H, oc, om, og);
     return hipGetLastError();
 }
 

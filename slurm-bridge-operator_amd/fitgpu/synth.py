@@ -215,24 +215,28 @@ CONFIGS = {
 C5_SLOTS, C5_SLOT_MIN = 1024, 5  # 1,024 slots × 5 min = 85.3 h ≥ the longest walltime (2,880 min)
 
 
-def make_config(name: str, nodes: int | None = None, jobs: int | None = None):
-    """Synthetic cluster for BASELINE.json config ``name`` (optionally truncated for tests)."""
+def make_config(name: str, nodes: int | None = None, jobs: int | None = None, shard: int = 0):
+    """Synthetic cluster for BASELINE.json config ``name`` (optionally truncated for tests).
+    ``shard`` s > 0 draws the s-th disjoint slice of the same streams (nodes [s*n, (s+1)*n), jobs
+    [s*j, (s+1)*j)): an independent cluster of the same shape, for weak-scaling runs."""
     n, j, p, gh, mn = CONFIGS[name]
     seed = SEEDS[name]
     n = n if nodes is None else nodes
     j = j if jobs is None else jobs
-    return gen_nodes(seed, n, p, gh), gen_jobs(seed, j, p, mn), gen_partitions(seed, p)
+    return (gen_nodes(seed, n, p, gh, start=shard * n), gen_jobs(seed, j, p, mn, start=shard * j),
+            gen_partitions(seed, p))
 
 
-def make_c5(nodes: int | None = None, jobs: int | None = None):
+def make_c5(nodes: int | None = None, jobs: int | None = None, shard: int = 0):
     """C5 (BASELINE.json config 5): C3's cluster shape plus the release timeline of the running
     jobs over a 1,024-slot horizon.  Returns (nodes, timeline, jobs, partitions)."""
     n, j, p, gh, mn = CONFIGS["c5"]
     seed = SEEDS["c5"]
     n = n if nodes is None else nodes
     j = j if jobs is None else jobs
-    return (gen_nodes(seed, n, p, gh), gen_releases(seed, n, C5_SLOTS, C5_SLOT_MIN, gh),
-            gen_jobs(seed, j, p, mn), gen_partitions(seed, p))
+    return (gen_nodes(seed, n, p, gh, start=shard * n),
+            gen_releases(seed, n, C5_SLOTS, C5_SLOT_MIN, gh, start=shard * n),
+            gen_jobs(seed, j, p, mn, start=shard * j), gen_partitions(seed, p))
 
 
 def make_c1():

@@ -1,0 +1,33 @@
+"""Diagnostic: cycle split of k_commit_tl (FIT_STAMPS build of the C5 commit; dev tool)."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "slurm-bridge-operator_amd")]
+from fitgpu import _lib  # noqa: E402
+_lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", "libfitgpu_stamps.so")
+from fitgpu import Engine, synth  # noqa: E402
+
+nn = int(sys.argv[1]) if len(sys.argv) > 1 else None
+jj = int(sys.argv[2]) if len(sys.argv) > 2 else None
+nodes, tline, jobs, parts = synth.make_c5(nn, jj)
+buf = (C.c_ulonglong * (64 * 12 + 8))()
+with Engine() as e:
+    e.load_nodes(nodes)
+    e.load_partitions(parts)
+    e.load_timeline(tline)
+    assert _lib.lib().fit_debug_tl_stamps(buf, 1) == 0
+    node, start, st = e.place_tl(jobs)
+    assert _lib.lib().fit_debug_tl_stamps(buf, 0) == 0
+print({k: st[k] for k in ("ms_total", "ms_scan", "ms_commit", "rounds", "stops_rescan", "stops_dirty", "placed")})
+tot = [sum(buf[c * 12 + i] for c in range(64)) for i in range(12)]
+j = max(tot[5], 1)
+names = ["clean", "dirty-eval", "new-dirty", "reserve", "tail"]
+print("cycles/job: " + ", ".join(f"{n} {tot[i] / j:.0f}" for i, n in enumerate(names)) +
+      f"; new dirty per job {tot[6] / j:.2f}; write-back per job {tot[7] / j:.0f}; jobs {tot[5]}")
+print(f"dirty-eval split: fast {tot[8] / j:.0f}, walk {tot[9] / j:.0f} (walks per job {tot[10] / j:.2f}), "
+      f"reduce {(tot[1] - tot[8] - tot[9]) / j:.0f}")
+sc = buf[64 * 12:64 * 12 + 8]
+print(f"scan: waves {sc[4]}, nodes/wave {sc[1] / max(sc[4], 1):.0f}, cycles/node {sc[0] / max(sc[1], 1):.0f}, "
+      f"long-walk batches/node {sc[2] / max(sc[1], 1):.2f}, nodes with > 4 runs {sc[3] / max(sc[1], 1):.2%}")
