@@ -34,6 +34,10 @@ hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* 
                             const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart, const uint16_t* jk,
                             int32_t nj, int32_t kmax, const int32_t* ptab, int32_t np,
                             int32_t* out, int8_t* jcomp);
+size_t joblists_scratch_ints(int32_t nj);
+hipError_t launch_joblists(hipStream_t st, const int8_t* jcomp, int32_t nj, int ncomp,
+                           int32_t* scratch, int32_t* g, int32_t* jb, int32_t* mb, int32_t* jl,
+                           int32_t* jpk);
 hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
                                const int32_t* gpu, const int32_t* av, const uint32_t* mask,
                                const int32_t* perm, int32_t nn, NodeRec* rec);
@@ -216,8 +220,8 @@ struct fit_ctx {
     DBuf<CommitResult> res;
     HBuf<CompPlan> h_plan;
     HBuf<CommitResult> h_res;
-    HBuf<int8_t> h_jcomp;
-    std::vector<int32_t> h_jl, h_jpk;
+    DBuf<int32_t> jls;    // device job-list scratch (block counts, counters, offsets)
+    HBuf<int32_t> h_jls;
 
     // time-windowed backfill: per-node run lists, built from the node
     // table + release events by fit_load_timeline
@@ -252,7 +256,8 @@ struct fit_ctx {
         res.release();
         h_plan.release();
         h_res.release();
-        h_jcomp.release();
+        jls.release();
+        h_jls.release();
         h_x.release();
         xcount.release();
         h_count.release();
@@ -468,40 +473,25 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     return 0;
 }
 
-// Per-component job lists in priority order (stable) from the prefilter's component ids
-// (h_jcomp, on the host); uploads jl / jpk.  jb[k] .. jb[k+1] = component k's list range.
+// Per-component job lists in priority order (stable), built on the device from the prefilter's
+// component ids (launch_joblists: counting sort by component); only the component offsets and
+// two counters come back to the host.  jb[k] .. jb[k+1] = component k's list range.
 int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& jb) {
     const int C = c->ncomp;
-    jb.assign(C + 1, 0);
     hipStream_t st = c->st;
-    for (int32_t q = 0; q < J; ++q) {
-        int8_t k = c->h_jcomp.p[q];
-        if (k >= 0) jb[(k & 0x3f) + 1]++;
-        else if (k == -2) S.rejected++;
-        else if (k == -3) return fail(FIT_E_INVAL, "job %d: negative demand or nodes_k > kmax", q);
-    }
-    for (int k = 0; k < C; ++k) jb[k + 1] += jb[k];
-    const int32_t JA = jb[C];
-    c->h_jl.resize(std::max(JA, 1));
-    c->h_jpk.resize(JA + 1);  // multi-node jobs before each list position (persistent engine)
-    {
-        std::vector<int32_t> f(jb.begin(), jb.end() - 1);
-        for (int32_t q = 0; q < J; ++q) {
-            int8_t k = c->h_jcomp.p[q];
-            if (k >= 0) {
-                const int32_t at = f[k & 0x3f]++;
-                c->h_jl[at] = q;
-                c->h_jpk[at + 1] = (k & 0x40) ? 1 : 0;
-            }
-        }
-        c->h_jpk[0] = 0;
-        for (int32_t i = 0; i < JA; ++i) c->h_jpk[i + 1] += c->h_jpk[i];
-    }
-    if (c->jl.ensure(std::max(JA, 1)) || c->jpk.ensure(JA + 1)) return FIT_E_OOM;
-    HIP_TRY(hipMemcpyAsync(c->jl.p, c->h_jl.data(), sizeof(int32_t) * JA, hipMemcpyHostToDevice,
-                           st));
-    HIP_TRY(hipMemcpyAsync(c->jpk.p, c->h_jpk.data(), sizeof(int32_t) * (JA + 1),
-                           hipMemcpyHostToDevice, st));
+    if (c->jl.ensure(std::max(J, 1)) || c->jpk.ensure(J + 1) ||
+        c->jls.ensure(std::max<size_t>(joblists_scratch_ints(J), 1) + 2 * (C + 1) + 2) ||
+        c->h_jls.ensure(C + 1 + 2))
+        return FIT_E_OOM;
+    int32_t* g = c->jls.p + joblists_scratch_ints(J);
+    int32_t* jbd = g + 2;
+    int32_t* mbd = jbd + C + 1;
+    HIP_TRY(launch_joblists(st, c->jcomp.p, J, C, c->jls.p, g, jbd, mbd, c->jl.p, c->jpk.p));
+    HIP_TRY(hipMemcpyAsync(c->h_jls.p, g, sizeof(int32_t) * (C + 3), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_jls.p[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
+    S.rejected = c->h_jls.p[0];
+    jb.assign(c->h_jls.p + 2, c->h_jls.p + 2 + C + 1);
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
     return 0;
 }
@@ -516,11 +506,9 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     S.jobs = J;
     hipStream_t st = c->st;
     // 1. prefilter: out[] init, FIT_REJECTED, component per job
-    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    if (c->jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
     HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
                              c->jcomp.p));
-    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     // 2. per-component job lists in priority order (stable)
     const int C = c->ncomp;
     std::vector<int32_t> jb;
@@ -685,12 +673,10 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     memset(&S, 0, sizeof S);
     S.jobs = J;
     hipStream_t st = c->st;
-    if (c->jcomp.ensure(std::max(J, 1)) || c->h_jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    if (c->jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
     HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nullptr, J, 1, c->d_ptab.p, c->np, out,
                              c->jcomp.p));
     if (J > 0) HIP_TRY(hipMemsetAsync(outs, 0xff, sizeof(int32_t) * J, st));
-    HIP_TRY(hipMemcpyAsync(c->h_jcomp.p, c->jcomp.p, J, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     const int C = c->ncomp;
     std::vector<int32_t> jb;
     int rc = build_job_lists(c, J, S, jb);

@@ -105,6 +105,142 @@ __global__ void k_scatter_nodes(const NodeRec* __restrict__ rec, int32_t nn,
     if (r.gpu >= 0) gpu[r.orig] = r.gpu;
 }
 
+
+// ------------------------------------------------------------------- device job lists
+// Per-component job lists in priority order (stable counting sort by component over the
+// prefilter's ids), plus jpk (multi-node jobs before each list position) — DESIGN.md §3.1.
+// Three passes over blocks of JL_BLOCK jobs: per-(block, component) counts by wave ballots, an
+// exclusive scan over blocks per component, and the scatter (block offset + wave offset + lane
+// rank), so the order inside each component is the caller's.
+constexpr int JL_BLOCK = 1024;
+constexpr int JL_MAXC = 32;
+
+__global__ __launch_bounds__(JL_BLOCK) void k_jl_count(const int8_t* __restrict__ jcomp, int32_t nj,
+                                                       int ncomp, int32_t* __restrict__ bc,
+                                                       int32_t* __restrict__ bm,
+                                                       int32_t* __restrict__ g) {
+    __shared__ int32_t wc[JL_BLOCK / 64][JL_MAXC], wm[JL_BLOCK / 64][JL_MAXC];
+    const int q = blockIdx.x * JL_BLOCK + threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k = q < nj ? jcomp[q] : -1;
+    const int comp = k >= 0 ? (k & 0x3f) : -1;
+    const bool multi = k >= 0 && (k & 0x40);
+    for (int cc = 0; cc < ncomp; ++cc) {
+        const uint64_t m = __ballot(comp == cc), mm = __ballot(comp == cc && multi);
+        if (lane == 0) {
+            wc[wave][cc] = __popcll(m);
+            wm[wave][cc] = __popcll(mm);
+        }
+    }
+    const uint64_t rj = __ballot(k == -2), bad = __ballot(k == -3);
+    if (lane == 0 && rj) atomicAdd(&g[0], (int)__popcll(rj));
+    if (lane == 0 && bad) atomicOr(&g[1], 1);
+    __syncthreads();
+    if ((int)threadIdx.x < ncomp) {
+        int a = 0, b = 0;
+        for (int w = 0; w < JL_BLOCK / 64; ++w) {
+            a += wc[w][threadIdx.x];
+            b += wm[w][threadIdx.x];
+        }
+        bc[blockIdx.x * JL_MAXC + threadIdx.x] = a;
+        bm[blockIdx.x * JL_MAXC + threadIdx.x] = b;
+    }
+}
+
+// exclusive scan over blocks per component (32 row-chunks × 32 components on 1024 threads), then
+// the component offsets jb / mb (C + 1 each)
+__global__ __launch_bounds__(1024) void k_jl_scan(int nblocks, int ncomp, int32_t* __restrict__ bc,
+                                                  int32_t* __restrict__ bm, int32_t* __restrict__ jb,
+                                                  int32_t* __restrict__ mb) {
+    __shared__ int32_t pa[32][JL_MAXC + 1], pb[32][JL_MAXC + 1];
+    const int cc = threadIdx.x & 31, r = threadIdx.x >> 5;
+    const int chunk = (nblocks + 31) / 32, i0 = r * chunk, i1 = min(nblocks, i0 + chunk);
+    int a = 0, b = 0;
+    if (cc < ncomp)
+        for (int i = i0; i < i1; ++i) {
+            a += bc[i * JL_MAXC + cc];
+            b += bm[i * JL_MAXC + cc];
+        }
+    pa[r][cc] = a;
+    pb[r][cc] = b;
+    __syncthreads();
+    if (threadIdx.x < 32) {  // per component: exclusive over the 32 chunks; totals in row 32
+        int x = 0, y = 0;
+        for (int k = 0; k < 32; ++k) {
+            const int u = pa[k][cc], v = pb[k][cc];
+            pa[k][cc] = x;
+            pb[k][cc] = y;
+            x += u;
+            y += v;
+        }
+        pa[0][JL_MAXC] = 0;  // unused
+        if (cc < ncomp) {
+            jb[cc] = x;  // component total for now
+            mb[cc] = y;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // component offsets from totals
+        int x = 0, y = 0;
+        for (int k = 0; k < ncomp; ++k) {
+            const int u = jb[k], v = mb[k];
+            jb[k] = x;
+            mb[k] = y;
+            x += u;
+            y += v;
+        }
+        jb[ncomp] = x;
+        mb[ncomp] = y;
+    }
+    if (cc < ncomp) {
+        a = pa[r][cc];
+        b = pb[r][cc];
+        for (int i = i0; i < i1; ++i) {
+            const int u = bc[i * JL_MAXC + cc], v = bm[i * JL_MAXC + cc];
+            bc[i * JL_MAXC + cc] = a;
+            bm[i * JL_MAXC + cc] = b;
+            a += u;
+            b += v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(JL_BLOCK) void k_jl_scatter(
+    const int8_t* __restrict__ jcomp, int32_t nj, int ncomp, const int32_t* __restrict__ bc,
+    const int32_t* __restrict__ bm, const int32_t* __restrict__ jb, const int32_t* __restrict__ mb,
+    int32_t* __restrict__ jl, int32_t* __restrict__ jpk) {
+    __shared__ int32_t wc[JL_BLOCK / 64][JL_MAXC], wm[JL_BLOCK / 64][JL_MAXC];
+    const int q = blockIdx.x * JL_BLOCK + threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k = q < nj ? jcomp[q] : -1;
+    const int comp = k >= 0 ? (k & 0x3f) : -1;
+    const bool multi = k >= 0 && (k & 0x40);
+    int rank = 0, mrank = 0;
+    for (int cc = 0; cc < ncomp; ++cc) {
+        const uint64_t m = __ballot(comp == cc), mm = __ballot(comp == cc && multi);
+        if (lane == 0) {
+            wc[wave][cc] = __popcll(m);
+            wm[wave][cc] = __popcll(mm);
+        }
+        if (comp == cc) {
+            rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            mrank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
+        }
+    }
+    __syncthreads();
+    if (comp >= 0) {
+        int wo = 0, wmo = 0;
+        for (int w = 0; w < wave; ++w) {
+            wo += wc[w][comp];
+            wmo += wm[w][comp];
+        }
+        const int pos = jb[comp] + bc[blockIdx.x * JL_MAXC + comp] + wo + rank;
+        const int before = mb[comp] + bm[blockIdx.x * JL_MAXC + comp] + wmo + mrank;
+        jl[pos] = q;
+        jpk[pos + 1] = before + (multi ? 1 : 0);
+    }
+    if (q == 0) jpk[0] = 0;
+}
 }  // namespace fitgpu
 
 // ---------------------------------------------------------------- host launch wrappers
@@ -149,6 +285,32 @@ hipError_t launch_prefilter(hipStream_t st, const int32_t* jcpu, const int32_t* 
     if (nj == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prefilter, dim3((nj + 255) / 256), dim3(256), 0, st, jcpu, jmem, jgpu, jwall,
                        jpart, jk, nj, kmax, ptab, np, out, jcomp);
+    return hipGetLastError();
+}
+
+// scratch: bc, bm = nblocks * JL_MAXC ints each; g = 2 ints (zeroed here); jb, mb = ncomp + 1
+size_t joblists_scratch_ints(int32_t nj) { return (size_t)2 * ((nj + JL_BLOCK - 1) / JL_BLOCK) * JL_MAXC; }
+
+hipError_t launch_joblists(hipStream_t st, const int8_t* jcomp, int32_t nj, int ncomp,
+                           int32_t* scratch, int32_t* g, int32_t* jb, int32_t* mb, int32_t* jl,
+                           int32_t* jpk) {
+    if (ncomp > JL_MAXC) return hipErrorInvalidValue;
+    const int nblocks = (nj + JL_BLOCK - 1) / JL_BLOCK;
+    int32_t* bc = scratch;
+    int32_t* bm = scratch + (size_t)nblocks * JL_MAXC;
+    hipError_t e = hipMemsetAsync(g, 0, 2 * sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    if (nj > 0) {
+        hipLaunchKernelGGL(k_jl_count, dim3(nblocks), dim3(JL_BLOCK), 0, st, jcomp, nj, ncomp, bc, bm, g);
+    }
+    hipLaunchKernelGGL(k_jl_scan, dim3(1), dim3(1024), 0, st, nblocks, ncomp, bc, bm, jb, mb);
+    if (nj > 0) {
+        hipLaunchKernelGGL(k_jl_scatter, dim3(nblocks), dim3(JL_BLOCK), 0, st, jcomp, nj, ncomp, bc,
+                           bm, jb, mb, jl, jpk);
+    } else {
+        e = hipMemsetAsync(jpk, 0, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
