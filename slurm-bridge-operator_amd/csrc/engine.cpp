@@ -401,7 +401,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         }
     const int nc = (int)comps.size();
     if (nc == 0) return 0;
-    const int64_t wcap = c->wmax;
+    const int64_t wcap = std::min(c->wmax, 8192);  // k_engine's per-tile counters: 128 job tiles
     const int64_t per_comp_cand = wcap * MAX_SLICES * KS;
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
         c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
@@ -421,8 +421,8 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.jend = jb[k + 1];
         s.cand_off = (int64_t)i * per_comp_cand;
         s.slot0 = (int32_t)(i * wcap);
-        s.wmin = c->wmin;
-        s.wmax = c->wmax;
+        s.wmin = std::min(c->wmin, (int)wcap);
+        s.wmax = (int32_t)wcap;
     }
     const size_t lds = engine_lds_bytes(maxnodes);
     int per_cu = engine_blocks_per_cu(lds);

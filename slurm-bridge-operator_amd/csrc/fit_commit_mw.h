@@ -104,6 +104,36 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void cbar() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
 
+// Tile readiness: the window's scan tiles complete while the window is being
+// committed; a helper waits for the (job tile)'s per-tile counter to reach nslice before reading
+// that tile's candidates, bound and job row — with agent-scope (L1-bypassing) loads, since the
+// committer's CU may hold stale lines of these reused buffers.  tdone == nullptr: the whole
+// window was acquired before the commit (no waits).
+struct MwTiles {
+    const unsigned* tdone;  // per-tile completed slice counts of this component's window
+    unsigned need;          // nslice
+};
+
+__device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ JobRec ld_agent_job(const JobRec* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t a = ld_agent_u64(q), b = ld_agent_u64(q + 1), c = ld_agent_u64(q + 2),
+                   d = ld_agent_u64(q + 3);
+    JobRec r;
+    r.q = (int32_t)(uint32_t)a;
+    r.cpu = (int32_t)(a >> 32);
+    r.mem = (int32_t)(uint32_t)b;
+    r.gpu = (int32_t)(b >> 32);
+    r.wall = (int32_t)(uint32_t)c;
+    r.pbit = (uint32_t)(c >> 32);
+    r.k = (int32_t)(uint32_t)d;
+    r.pad = (int32_t)(d >> 32);
+    return r;
+}
+
 // a VGPR zero the compiler cannot see through: keeps uniform loads of data written by other
 // workgroups in this launch on the vector path (vmcnt, in order) instead of the scalar cache
 __device__ __forceinline__ int opaque_zero() {
@@ -120,6 +150,26 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
     const uint32_t sc = (min((uint32_t)dg, 255u) << 24) | (min((uint32_t)dc, 4095u) << 12) |
                         min((uint32_t)dm >> 10, 4095u);
     return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
+}
+
+// Wait until job tt's scan tile is complete (uniform; `ready` = tiles known complete, they finish
+// roughly in order).  false: the decider halted / a watchdog tripped.
+__device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& ready, MwShared* S) {
+    if (!T.tdone) return true;
+    const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
+    if (tile < ready) return true;
+    for (unsigned sp = 0;; ++sp) {
+        if (__hip_atomic_load(T.tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= T.need)
+            break;
+        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
+        if (sp > MW_SPIN_LIMIT) {
+            lds_st(&S->fail, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    ready = tile + 1;
+    return true;
 }
 
 // ------------------------------------------------------------------------------- helper
@@ -142,9 +192,16 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
         }                                                                                      \
         {                                                                                      \
             const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
-            kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                             \
-            jr[C] = wjob[P.slot0 + tt_];                                                       \
-            jbd[C] = bnd[P.slot0 + tt_];                                                       \
+            if (!mw_tile_ready(T, tt_, ready, S)) goto hdone;                                  \
+            if (T.tdone) {                                                                     \
+                kk[C] = has ? ld_agent_u64(cand + eoff + (int64_t)tt_ * E) : KEY_INF;          \
+                jr[C] = ld_agent_job(wjob + P.slot0 + tt_);                                    \
+                jbd[C] = ld_agent_u64(bnd + P.slot0 + tt_);                                    \
+            } else {                                                                           \
+                kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                         \
+                jr[C] = wjob[P.slot0 + tt_];                                                   \
+                jbd[C] = bnd[P.slot0 + tt_];                                                   \
+            }                                                                                  \
         }                                                                                      \
         /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs */                  \
         uint32_t v_;                                                                           \
@@ -234,7 +291,7 @@ __device__ __noinline__ void mw_helper(const CompPlan& P, MwShared* S,
                                           const NodeRec* __restrict__ rec,
                                           const uint64_t* __restrict__ cand,
                                           const uint64_t* __restrict__ bnd,
-                                          const JobRec* __restrict__ wjob, int h) {
+                                          const JobRec* __restrict__ wjob, int h, MwTiles T) {
     const int lane = threadIdx.x & 63;
     const int E = P.nslice * KS;
     const bool has = lane < E;
@@ -247,12 +304,20 @@ __device__ __noinline__ void mw_helper(const CompPlan& P, MwShared* S,
     JobRec jr[3];
     int32_t rc[3], rm[3], rg[3], ra[3], ro[3];
     uint32_t rk[3];
+    int ready = 0;  // scan tiles known complete
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // jobs t and t + H
         const int tt = min(t + s * MW_H, wlast) + z;
-        kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
-        jr[s] = wjob[P.slot0 + tt];
-        jbd[s] = bnd[P.slot0 + tt];
+        if (!mw_tile_ready(T, tt, ready, S)) return;  // halted / watchdog
+        if (T.tdone) {
+            kk[s] = has ? ld_agent_u64(cand + eoff + (int64_t)tt * E) : KEY_INF;
+            jr[s] = ld_agent_job(wjob + P.slot0 + tt);
+            jbd[s] = ld_agent_u64(bnd + P.slot0 + tt);
+        } else {
+            kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
+            jr[s] = wjob[P.slot0 + tt];
+            jbd[s] = bnd[P.slot0 + tt];
+        }
     }
     {
         const uint32_t p = kk[0] != KEY_INF ? (uint32_t)kk[0] : (uint32_t)P.nb;
@@ -494,7 +559,8 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
                                                          const uint64_t* __restrict__ cand,
                                                          const uint64_t* __restrict__ bnd,
                                                          const JobRec* __restrict__ wjob,
-                                                         int32_t* __restrict__ out, int kmax) {
+                                                         int32_t* __restrict__ out, int kmax,
+                                                         MwTiles T = MwTiles{nullptr, 0u}) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
@@ -515,9 +581,9 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
             S->res[3] = r.placed;
         }
     } else if (MW_H == MW_WAVES - 1) {
-        mw_helper(P, S, rec, cand, bnd, wjob, wave);
+        mw_helper(P, S, rec, cand, bnd, wjob, wave, T);
     } else if (wave != 4) {
-        mw_helper(P, S, rec, cand, bnd, wjob, wave < 4 ? wave : wave - 1);
+        mw_helper(P, S, rec, cand, bnd, wjob, wave < 4 ? wave : wave - 1, T);
     }
     __syncthreads();
     const CommitResult r{S->res[0], S->res[1], S->res[2], S->res[3]};

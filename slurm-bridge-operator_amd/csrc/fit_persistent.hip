@@ -22,6 +22,7 @@
 namespace fitgpu {
 
 constexpr unsigned QCAP = 1u << 16;  // task ring entries (8-byte {epoch, tile} granules)
+constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
 constexpr unsigned SPIN_LIMIT = 1u << 25;
 constexpr unsigned long long TASK_EXIT = ~0ull;
 
@@ -34,6 +35,7 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned error;     // 1 = watchdog
     unsigned pad2[30];
     unsigned done[32][32];  // per component tiles completed (own 128-B line each)
+    unsigned tdone[32][ENGINE_TILES];  // per component, per window job tile: slices completed
 };
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
@@ -51,6 +53,15 @@ __device__ __forceinline__ void release_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
+}
+
+// Spin (wave 0 of a committer) until component c has completed `target` scan tiles in total.
+__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, unsigned target) {
+    for (unsigned spins = 0; ld_agent(&ctl->done[c][0]) < target;) {
+        if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
 }
 
 // Windows holding a multi-node job: the single-wave commit (fit_common.h), kept out of line so
@@ -103,11 +114,22 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             P.cand_off = S.cand_off;
             P.slot0 = S.slot0;
             int64_t t0 = 0;
+            // a window holding a multi-node job is committed by wave 0 alone (commit_window
+            // handles k > 1) after its whole scan; the decider/helper pipeline covers k = 1
+            // windows and starts at once: helpers wait per job tile (MwTiles)
+            const bool multi = jpk[cursor + w] != jpk[cursor];
             if (wave == 0) {
+                t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                // the previous round's tiles (also those past its stop) must all be complete
+                // before their buffers and counters are reused
+                bool fail = !wait_tiles(ctl, c, target);
+                const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 if (lane == 0) plans[c] = P;
                 for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
-                release_agent();  // plan, bound reset and last round's node rows → visible
-                const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
+                for (unsigned i = lane; i < ntj; i += 64)
+                    __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                release_agent();  // plan, bound / counter reset and last round's node rows → visible
+                const unsigned ntiles = ntj * (unsigned)S.nslice;
                 unsigned base = 0;
                 if (lane == 0)
                     base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
@@ -122,18 +144,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
                 target += ntiles;
-                t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-                unsigned spins = 0;
-                bool fail = false;
-                while (ld_agent(&ctl->done[c][0]) < target) {
-                    if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) {
-                        fail = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
+                if (multi && !fail) fail = !wait_tiles(ctl, c, target);
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
-                acquire_agent();  // candidates, bounds, window job rows of this round (CU-wide)
+                acquire_agent();  // node rows written by this block: CU-wide view for all waves
                 if (lane == 0) s_fail = fail;
             }
             __syncthreads();
@@ -142,8 +155,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // a window holding a multi-node job is committed by wave 0 alone (commit_window
             // handles k > 1); the decider/helper pipeline covers k = 1 windows
             CommitResult R;
-            if (jpk[cursor + w] == jpk[cursor]) {
-                R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax);
+            if (!multi) {
+                R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax,
+                                     MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice});
             } else {
                 if (wave == 0) {
                     const CommitResult r0 =
@@ -233,6 +247,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         __syncthreads();
         if (threadIdx.x == 0) {
             release_agent();
+            __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
