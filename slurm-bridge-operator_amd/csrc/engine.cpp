@@ -72,6 +72,16 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg*
                             int64_t rank_stride, int nranks, const uint64_t* bnd,
                             const JobRec* wjob, const int32_t* perm, int32_t* out, int32_t* outs,
                             CommitResult* res, int32_t H, int32_t R);
+int engine_tl_runs(int32_t max_component_nodes);
+size_t engine_tl_lds_bytes(int32_t max_component_nodes);
+int engine_tl_blocks_per_cu(size_t lds);
+hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
+                            const void* cs, void* co, CompPlan* plans, int ncomp, Seg* slab,
+                            TlHdr* hdr, const int32_t* jl, const int32_t* jcpu,
+                            const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
+                            const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
+                            const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
+                            int32_t slot_min, int32_t R, int64_t* wbusy);
 hipError_t launch_expand_tl(hipStream_t st, const int32_t* perm, const Seg* slab,
                             const TlHdr* hdr, int32_t nn, int32_t H, int32_t* oc, int32_t* om,
                             int32_t* og);
@@ -665,6 +675,97 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
 // scans / commits (fit_timeline.hip).  world > 1 always splits by nodes: every rank scans its
 // share of each component, the candidate sections are exchanged each round and the identical
 // deterministic commit runs on every rank over replicated run lists.
+// Persistent single-launch backfill (k_engine_tl): the placement's rounds for
+// every component in one launch, no host round trips (world == 1).
+int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t* cpu,
+                      const int32_t* mem, const int32_t* gpu, const int32_t* wall,
+                      const uint16_t* part, int32_t* out, int32_t* outs, fit_stats& S) {
+    const int C = c->ncomp;
+    hipStream_t st = c->st;
+    std::vector<int> comps;
+    int32_t maxnodes = 0;
+    for (int k = 0; k < C; ++k)
+        if (jb[k + 1] > jb[k]) {
+            comps.push_back(k);
+            maxnodes = std::max(maxnodes, c->nb[k + 1] - c->nb[k]);
+        }
+    const int nc = (int)comps.size();
+    if (nc == 0) return 0;
+    const int R = engine_tl_runs(maxnodes);
+    if (R < 1) return fail(FIT_E_INVAL, "partition component of %d nodes is too large for the "
+                                        "timeline engine's LDS", maxnodes);
+    const int64_t wcap = std::min(c->wmax, 8192);
+    int slices = TL_SLICES, tl_min_sub = TL_MIN_SUB;
+    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 4));
+    if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
+    const int64_t per_comp_cand = wcap * slices * KS;
+    if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
+        c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
+        c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
+        c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
+        c->h_err.ensure(4))
+        return FIT_E_OOM;
+    for (int i = 0; i < nc; ++i) {
+        const int k = comps[i];
+        CompState& s = c->h_ecs.p[i];
+        s.nb = s.sb = c->nb[k];
+        s.ne = s.se = c->nb[k + 1];
+        const int32_t len = s.ne - s.nb;
+        s.sub = std::max(tl_min_sub, (len + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
+        s.nslice = std::max(1, (len + SCAN_WAVES * s.sub - 1) / (SCAN_WAVES * s.sub));
+        s.jstart = jb[k];
+        s.jend = jb[k + 1];
+        s.cand_off = (int64_t)i * per_comp_cand;
+        s.slot0 = (int32_t)(i * wcap);
+        s.wmin = std::min(c->wmin, (int)wcap);
+        s.wmax = (int32_t)wcap;
+    }
+    const size_t lds = engine_tl_lds_bytes(maxnodes);
+    const int per_cu = engine_tl_blocks_per_cu(lds);
+    if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine_tl does not fit on a CU (lds %zu)", lds);
+    int workers = std::max(8, per_cu * c->cus - nc);
+    if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
+    if (c->ebusy.ensure(workers) || c->h_ebusy.ensure(workers)) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
+    HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    HIP_TRY(launch_engine_tl(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
+                             c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
+                             part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
+                             c->tl_slots, c->tl_slot_min, R, c->ebusy.p));
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * workers,
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_err.p[0]) return fail(FIT_E_HIP, "timeline engine watchdog tripped (code %u)", c->h_err.p[0]);
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    S.ms_device += ms;
+    int64_t busy = 0;
+    for (int i = 0; i < workers; ++i) busy += c->h_ebusy.p[i];
+    S.ms_scan += busy / 1e5 / workers;
+    double commit_max = 0;
+    for (int i = 0; i < nc; ++i) {
+        const CompOut& o = c->h_eco.p[i];
+        const int k = comps[i];
+        if (o.done_jobs != jb[k + 1] - jb[k])
+            return fail(FIT_E_HIP, "component %d resolved %lld of %d jobs", k, (long long)o.done_jobs,
+                        jb[k + 1] - jb[k]);
+        S.evals += o.evals;
+        S.placed += o.placed;
+        S.rounds = std::max<int64_t>(S.rounds, o.rounds);
+        S.stops_rescan += o.stops_rescan;
+        S.stops_dirty += o.stops_dirty;
+        commit_max = std::max(commit_max, o.t_commit / 1e5);
+    }
+    S.ms_commit += commit_max;
+    S.engine = 1;
+    return 0;
+}
+
 int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
                   const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out,
                   int32_t* outs, fit_stats* stats) {
@@ -685,6 +786,14 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     const int shards = c->world, srank = c->rank;
     S.shard_mode = node_sharded ? FIT_SHARD_NODES : 0;
     S.components = C;
+    if (c->persistent && !node_sharded) {
+        rc = run_persistent_tl(c, jb, cpu, mem, gpu, wall, part, out, outs, S);
+        if (rc) return rc;
+        S.unplaced = J - S.placed - S.rejected;
+        S.ms_total = now_ms() - t0;
+        if (stats) *stats = S;
+        return 0;
+    }
     std::vector<int32_t> cur(jb.begin(), jb.end() - 1), win(C, c->wmin);
     if (c->plan.ensure(C + 1) || c->res.ensure(C + 1) || c->h_plan.ensure(C + 1) ||
         c->h_res.ensure(C + 1))

@@ -61,8 +61,11 @@ struct CompOut {
 
 // ---- SPEC §2b time-windowed backfill (fit_timeline.hip) --------------------
 constexpr int TL_MAX_SLOTS = 1024;  // horizon limit (slots); the C5 horizon
-constexpr int TL_UCAP = 64;         // dirty nodes per component per round (one per lane)
-constexpr int TL_SLICES = 16;       // block-slices per job (over all ranks) in the timeline scan
+#ifndef TL_UCAP_DEF
+#define TL_UCAP_DEF 64
+#endif
+constexpr int TL_UCAP = TL_UCAP_DEF;  // dirty nodes per component per round (TL_UCAP / 64 per lane)
+constexpr int TL_SLICES = 4;        // block-slices per job (over all ranks) in the timeline scan
 constexpr int TL_MIN_SUB = 32;      // minimum nodes per wave sub-slice in the timeline scan
 constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position
 constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;

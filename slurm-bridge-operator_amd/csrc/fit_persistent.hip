@@ -18,51 +18,9 @@
 #include <algorithm>
 
 #include "fit_commit_mw.h"
+#include "fit_engine_ctl.h"
 
 namespace fitgpu {
-
-constexpr unsigned QCAP = 1u << 16;  // task ring entries (8-byte {epoch, tile} granules)
-constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
-constexpr unsigned SPIN_LIMIT = 1u << 25;
-constexpr unsigned long long TASK_EXIT = ~0ull;
-
-struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
-    unsigned q_tail;   // tiles reserved by committers
-    unsigned pad0[31];
-    unsigned q_head;   // tiles claimed by workers
-    unsigned pad1[31];
-    unsigned finished;  // components done
-    unsigned error;     // 1 = watchdog
-    unsigned pad2[30];
-    unsigned done[32][32];  // per component tiles completed (own 128-B line each)
-    unsigned tdone[32][ENGINE_TILES];  // per component, per window job tile: slices completed
-};
-
-__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void acquire_agent() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_dcache_inv();  // scalar cache: node rows, plans, job rows are s_loaded
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-__device__ __forceinline__ void release_agent() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
-}
-
-// Spin (wave 0 of a committer) until component c has completed `target` scan tiles in total.
-__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, unsigned target) {
-    for (unsigned spins = 0; ld_agent(&ctl->done[c][0]) < target;) {
-        if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-}
 
 // Windows holding a multi-node job: the single-wave commit (fit_common.h), kept out of line so
 // its registers are allocated apart from the decider / helper / worker loops.

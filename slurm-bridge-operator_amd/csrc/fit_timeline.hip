@@ -7,17 +7,19 @@
 // ceilings, partition mask, first TL_HEAD runs) that the scan streams.  The speculative rounds are
 // the plain fit's (fit_common.h): k_scan_tl keeps the exact top-KS keys per (job, block-slice)
 // plus a bound against the round-start timelines; k_commit_tl walks the window in priority order
-// with a dirty set of at most TL_UCAP nodes (one per lane) whose run lists (and prefix minima)
+// with a dirty set of at most TL_UCAP nodes (two per lane) whose run lists (and prefix minima)
 // live in LDS, re-evaluates them exactly per job and reserves each decision in place.
 //   key = start << 54 | score << 22 | position   (earliest start, then best fit, then node)
 // The sequential semantics reproduced bit-exactly is oracle/fitref_tl.c:ref_place_tl.
 #include <algorithm>
 
 #include "fit_common.h"
+#include "fit_engine_ctl.h"
 
 namespace fitgpu {
 
 constexpr int TL_PM_STEPS = 32;     // LDS run lists hold <= 2 * TL_PM_STEPS = 64 runs
+constexpr int TL_UPL = TL_UCAP / 64;  // dirty slots per lane
 constexpr int32_t TL_BIG = 0x7fffffff;
 
 #ifdef FIT_STAMPS
@@ -99,6 +101,25 @@ __device__ __forceinline__ uint64_t tl_eval(const Seg* sg, int cnt, bool live, i
             const Seg g = sg[i];
             tl_step(w, g.end, g.cpu, g.mem, g.gpu, jc, jm, jg, d, H, lim, pos);
         }
+    }
+    return w.key;
+}
+
+// Same walk, four runs per step (one round trip for four reads, one ballot per four runs).
+// `cap`: readable entries behind sg (reads past the list are clamped into it and masked).
+__device__ __forceinline__ uint64_t tl_eval4(const Seg* sg, int cnt, int cap, bool live, int32_t jc,
+                                             int32_t jm, int32_t jg, int32_t d, int32_t H,
+                                             uint32_t pos, uint64_t cut) {
+    const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
+    TlWalk w{-1, 0, 0, 0, 0, KEY_INF, live && d <= H};
+    for (int i = 0;; i += 4) {
+        if (!__ballot(w.live && i < cnt)) break;
+        Seg g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = sg[min(i + u, cap - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u < cnt) tl_step(w, g[u].end, g[u].cpu, g[u].mem, g[u].gpu, jc, jm, jg, d, H, lim, pos);
     }
     return w.key;
 }
@@ -205,19 +226,15 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
     if (w.key < key[KS - 1]) topk_insert(key, w.key);
 }
 
-__global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
-    const Seg* __restrict__ slab, const TlHdr* __restrict__ hdr,
-    const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
-    const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
-    const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
-    const CompPlan* __restrict__ plan, int ncomp, uint64_t* __restrict__ cand,
-    uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob, int32_t H, int32_t slot_min) {
-    __shared__ uint64_t xk[SCAN_WAVES / 2][KS][64];
-    const int c = find_comp(plan, ncomp, blockIdx.x);
-    const CompPlan P = plan[c];
-    const int local = blockIdx.x - P.blk0;
-    const int tile = __builtin_amdgcn_readfirstlane(local / P.nslice);
-    const int s = __builtin_amdgcn_readfirstlane(local - tile * P.nslice);
+// One scan tile: SCAN_JOBS window jobs × block-slice s of the component (host-driven k_scan_tl
+// and the persistent k_engine_tl workers).  xk: LDS merge buffer.
+__device__ __forceinline__ void scan_tile_tl(
+    const CompPlan& P, int tile, int s, const Seg* __restrict__ slab,
+    const TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
+    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[KS][64]) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -299,6 +316,23 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
                   (unsigned long long)key[KS - 1]);
     if (s == 0) wjob[P.slot0 + t] = J;
+}
+
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
+    const Seg* __restrict__ slab, const TlHdr* __restrict__ hdr,
+    const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
+    const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
+    const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
+    const CompPlan* __restrict__ plan, int ncomp, uint64_t* __restrict__ cand,
+    uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob, int32_t H, int32_t slot_min) {
+    __shared__ uint64_t xk[SCAN_WAVES / 2][KS][64];
+    const int c = find_comp(plan, ncomp, blockIdx.x);
+    const CompPlan P = plan[c];
+    const int local = blockIdx.x - P.blk0;
+    const int tile = __builtin_amdgcn_readfirstlane(local / P.nslice);
+    const int s = __builtin_amdgcn_readfirstlane(local - tile * P.nslice);
+    scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
+                 slot_min, xk);
 }
 
 // --------------------------------------------------------------------------- k_commit_tl
@@ -430,25 +464,21 @@ __device__ __forceinline__ int tl_reserve_lds(Seg* L, int n, int cap, int32_t s,
 // Per job, on the fast path, every wait is on LDS or on loads issued one job earlier: the job
 // stream (row, bound, candidate keys) is prefetched with vector loads (in-order vmcnt), and the
 // dirty evaluation, reservation and prefix-minimum update are LDS-only.
+// One component's window, by one wave (host-driven k_commit_tl and the persistent k_engine_tl
+// committers).  smem: commit_tl_lds_bytes() of LDS.
 template <int EPL>
-__global__ __launch_bounds__(64) void k_commit_tl(
-    Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const CompPlan* __restrict__ plan,
-    const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
+__device__ __forceinline__ CommitResult commit_tl_window(
+    const CompPlan& P, int c, unsigned char* smem, Seg* __restrict__ slab,
+    TlHdr* __restrict__ hdr, const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
     const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
     const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
-    CommitResult* __restrict__ res, int32_t H, int32_t R) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int32_t H, int32_t R) {
     Seg* scr = reinterpret_cast<Seg*>(smem);                // general-path scratch
     Seg* lr = scr + TL_MAX_SLOTS;                           // TL_UCAP regions of R runs
     int4* pmr = reinterpret_cast<int4*>(lr + TL_UCAP * R);  // their prefix minima
     uint32_t* bitmap = reinterpret_cast<uint32_t*>(pmr + TL_UCAP * R);
-    const int c = blockIdx.x;
-    const CompPlan P = plan[c];
     const int lane = threadIdx.x & 63;
-    if (P.w == 0) {
-        if (lane == 0) res[c] = CommitResult{0, 0, 0, 0};
-        return;
-    }
+    if (P.w == 0) return CommitResult{0, 0, 0, 0};
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
 
@@ -468,11 +498,22 @@ __global__ __launch_bounds__(64) void k_commit_tl(
     int nu = 0, placed = 0, stop = 0, t = 0;
     // this lane's dirty node (lane < nu): position, mask, id, run count, column ceilings, and
     // whether its list lives in the global slab instead of LDS
-    uint32_t upos = 0u, umask = 0u;
-    int32_t uorig = -1, ucnt = 0, ucc = -1, ucm = -1, ucg = -1;
-    bool uglob = false;
-    const Seg* const mine = lr + lane * R;
-    const int4* const pmine = pmr + lane * R;
+    // dirty slot u = i * 64 + lane, i < TL_UPL (register arrays indexed by literals / unrolled loops)
+    uint32_t upos[TL_UPL], umask[TL_UPL];
+    int32_t uorig[TL_UPL], ucnt[TL_UPL], ucc[TL_UPL], ucm[TL_UPL], ucg[TL_UPL];
+    bool uglob[TL_UPL];
+#pragma unroll
+    for (int i = 0; i < TL_UPL; ++i) {
+        upos[i] = umask[i] = 0u;
+        uorig[i] = -1;
+        ucnt[i] = 0;
+        ucc[i] = ucm[i] = ucg[i] = -1;
+        uglob[i] = false;
+    }
+    // the placement of job t is parked in lane t & 63 and stored 64 at a time (no store per job:
+    // on gfx9 stores count in vmcnt, and the next prefetch wait would wait for them)
+    int32_t oq = -1, on = -1, os = -1;
+
 #ifdef FIT_STAMPS
     unsigned long long tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -511,43 +552,62 @@ __global__ __launch_bounds__(64) void k_commit_tl(
         const uint64_t cw = wave_min_key(cm);
         TL_CLK(c1);
         TL_ACC(0, c0, c1);
-        const bool dl = lane < nu && (umask & jp) != 0u && jc <= ucc && jm <= ucm && jg <= ucg &&
-                        jd <= H;
         // LDS lists: a start at slot 0 through the prefix minima — k = the first run ending at or
         // after d, by a 4-ary search (three rounds of three independent reads); a later start
         // (only when it can still win) or a global list walks the runs
-        uint64_t dk = KEY_INF;
-        bool walk = dl && uglob;
-        if (dl && !uglob) {
-            int k = 0;
+        uint64_t dk[TL_UPL], dkm = KEY_INF;
+        bool walk[TL_UPL], anyw = false;
 #pragma unroll
-            for (int q = 16; q >= 1; q >>= 2) {
-                const int i1 = k + q - 1, i2 = k + 2 * q - 1, i3 = k + 3 * q - 1;
-                const int32_t x1 = i1 < ucnt ? mine[i1].end : TL_BIG;
-                const int32_t x2 = i2 < ucnt ? mine[i2].end : TL_BIG;
-                const int32_t x3 = i3 < ucnt ? mine[i3].end : TL_BIG;
-                k += q * ((x1 < jd) + (x2 < jd) + (x3 < jd));
+        for (int i = 0; i < TL_UPL; ++i) {
+            const bool dl = i * 64 + lane < nu && (umask[i] & jp) != 0u && jc <= ucc[i] &&
+                            jm <= ucm[i] && jg <= ucg[i] && jd <= H;
+            dk[i] = KEY_INF;
+            walk[i] = dl && uglob[i];
+            if (dl && !uglob[i]) {
+                const Seg* const mine = lr + (i * 64 + lane) * R;
+                int k = 0;
+#pragma unroll
+                for (int q = 16; q >= 1; q >>= 2) {
+                    // k + 3q - 1 <= 63: clamp into the region, read unconditionally (the three
+                    // reads issue together), mask past the list
+                    const int i1 = k + q - 1, i2 = k + 2 * q - 1, i3 = k + 3 * q - 1;
+                    const int32_t y1 = mine[min(i1, R - 1)].end, y2 = mine[min(i2, R - 1)].end,
+                                  y3 = mine[min(i3, R - 1)].end;
+                    const int32_t x1 = i1 < ucnt[i] ? y1 : TL_BIG;
+                    const int32_t x2 = i2 < ucnt[i] ? y2 : TL_BIG;
+                    const int32_t x3 = i3 < ucnt[i] ? y3 : TL_BIG;
+                    k += q * ((x1 < jd) + (x2 < jd) + (x3 < jd));
+                }
+                const int4 pk = pmr[(i * 64 + lane) * R + k];
+                if (pk.x >= jc && pk.y >= jm && pk.z >= jg)
+                    dk[i] = tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, upos[i]);
+                else
+                    walk[i] = cw == KEY_INF || (cw >> 54) > 0;
             }
-            const int4 pk = pmine[k];
-            if (pk.x >= jc && pk.y >= jm && pk.z >= jg)
-                dk = tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, upos);
-            else
-                walk = cw == KEY_INF || (cw >> 54) > 0;
+            anyw = anyw || walk[i];
         }
         TL_CLK(c1b);
         TL_ACC(8, c1, c1b);
-        if (__ballot(walk)) {
+        if (__ballot(anyw)) {
 #ifdef FIT_STAMPS
             tacc[10] += 1;
 #endif
-            const uint64_t wl = tl_eval(mine, ucnt, walk && !uglob, jc, jm, jg, jd, H, upos, cw);
-            const uint64_t wg = tl_eval(slab + (int64_t)upos * TL_MAX_SLOTS, ucnt, walk && uglob,
-                                        jc, jm, jg, jd, H, upos, cw);
-            dk = walk ? (uglob ? wg : wl) : dk;
+#pragma unroll
+            for (int i = 0; i < TL_UPL; ++i) {
+                if (!__ballot(walk[i])) continue;
+                const uint64_t wl = tl_eval4(lr + (i * 64 + lane) * R, ucnt[i], R,
+                                             walk[i] && !uglob[i], jc, jm, jg, jd, H, upos[i], cw);
+                const uint64_t wg = tl_eval4(slab + (int64_t)upos[i] * TL_MAX_SLOTS, ucnt[i],
+                                             TL_MAX_SLOTS, walk[i] && uglob[i], jc, jm, jg, jd, H,
+                                             upos[i], cw);
+                dk[i] = walk[i] ? (uglob[i] ? wg : wl) : dk[i];
+            }
         }
+#pragma unroll
+        for (int i = 0; i < TL_UPL; ++i) dkm = umin64(dkm, dk[i]);
         TL_CLK(c1c);
         TL_ACC(9, c1b, c1c);
-        const uint64_t best = umin64(cw, wave_min_key(dk));
+        const uint64_t best = umin64(cw, wave_min_key(dkm));
         TL_CLK(c2);
         TL_ACC(1, c1, c2);
         if (Bc != KEY_INF && best > Bc) {
@@ -557,10 +617,14 @@ __global__ __launch_bounds__(64) void k_commit_tl(
         int32_t node = -1, start = -1;
         if (best != KEY_INF) {
             const uint32_t pos = (uint32_t)best & TL_POS_MASK;
-            const uint64_t dm = __ballot(dk == best);
+            int l = -1;  // winning dirty slot
+#pragma unroll
+            for (int i = TL_UPL - 1; i >= 0; --i) {
+                const uint64_t dm = __ballot(dk[i] == best);
+                if (dm) l = i * 64 + __builtin_ctzll(dm);
+            }
             TL_CLK(c3);
-            int l;
-            if (dm == 0ull) {  // a clean candidate wins: it becomes dirty lane nu
+            if (l < 0) {  // a clean candidate wins: it becomes dirty slot nu
                 if (nu == TL_UCAP) {
                     stop = 2;
                     break;
@@ -575,16 +639,19 @@ __global__ __launch_bounds__(64) void k_commit_tl(
                     if (lane < n0) dst[lane] = src[lane];  // n0 <= R <= 64
                     tl_pm_build(dst, pmr + l * R, n0);
                 }
-                if (lane == l) {
-                    upos = pos;
-                    umask = h0.mask;
-                    uorig = perm[pos];
-                    ucnt = n0;
-                    ucc = h0.cpu;
-                    ucm = h0.mem;
-                    ucg = h0.gpu;
-                    uglob = g;
-                }
+                const int32_t o0 = perm[pos];
+#pragma unroll
+                for (int i = 0; i < TL_UPL; ++i)
+                    if (i * 64 + lane == l) {
+                        upos[i] = pos;
+                        umask[i] = h0.mask;
+                        uorig[i] = o0;
+                        ucnt[i] = n0;
+                        ucc[i] = h0.cpu;
+                        ucm[i] = h0.mem;
+                        ucg[i] = h0.gpu;
+                        uglob[i] = g;
+                    }
                 if (lane == 0) {
                     const uint32_t rel = pos - nb;
                     bitmap[rel >> 5] |= 1u << (rel & 31);
@@ -592,13 +659,19 @@ __global__ __launch_bounds__(64) void k_commit_tl(
 #ifdef FIT_STAMPS
                 tacc[6] += 1;
 #endif
-            } else {
-                l = __builtin_ctzll(dm);
             }
             TL_CLK(c4);
             TL_ACC(2, c3, c4);
-            const bool g = __builtin_amdgcn_readlane((int)uglob, l) != 0;
-            const int n = __builtin_amdgcn_readlane(ucnt, l);
+            const int li = l >> 6, ll = l & 63;
+            bool g = false;
+            int n = 0, orig = -1;
+#pragma unroll
+            for (int i = 0; i < TL_UPL; ++i)
+                if (i == li) {
+                    g = __builtin_amdgcn_readlane((int)uglob[i], ll) != 0;
+                    n = __builtin_amdgcn_readlane(ucnt[i], ll);
+                    orig = __builtin_amdgcn_readlane(uorig[i], ll);
+                }
             start = (int32_t)(best >> 54);
             int nn;
             if (!g) {
@@ -611,35 +684,60 @@ __global__ __launch_bounds__(64) void k_commit_tl(
                     if (lane < n) gl[lane] = L[lane];
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     nn = tl_reserve_any(gl, n, start, start + jd, jc, jm, jg, scr);
-                    if (lane == l) uglob = true;
+#pragma unroll
+                    for (int i = 0; i < TL_UPL; ++i)
+                        if (i * 64 + lane == l) uglob[i] = true;
                 }
             } else {
                 nn = tl_reserve_any(slab + (int64_t)pos * TL_MAX_SLOTS, n, start, start + jd, jc,
                                     jm, jg, scr);
             }
-            if (lane == l) ucnt = nn;
-            node = __builtin_amdgcn_readlane(uorig, l);
+#pragma unroll
+            for (int i = 0; i < TL_UPL; ++i)
+                if (i * 64 + lane == l) ucnt[i] = nn;
+            node = orig;
             ++placed;
             TL_CLK(c5);
             TL_ACC(3, c4, c5);
         }
         TL_CLK(c6);
-        if (lane == 0) {
-            out[jq] = node;
-            outs[jq] = start;
+        if (lane == (t & 63)) {
+            oq = jq;
+            on = node;
+            os = start;
+        }
+        if ((t & 63) == 63) {  // uniform
+            if (oq >= 0) {
+                out[oq] = on;
+                outs[oq] = os;
+            }
+            oq = -1;
         }
         TL_CLK(c7);
         TL_ACC(4, c6, c7);
+    }
+    if (oq >= 0 && lane < (t & 63)) {  // the last partial group
+        out[oq] = on;
+        outs[oq] = os;
     }
     TL_CLK(e0);
     // round end: LDS lists back to their slabs (the next scan reads them), headers for all
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // global-list writes before re-reads
     for (int l = 0; l < nu; ++l) {
-        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)upos, l);
-        const int n = __builtin_amdgcn_readlane(ucnt, l);
+        const int li = l >> 6, ll = l & 63;
+        uint32_t p = 0;
+        int n = 0;
+        bool gl = false;
+#pragma unroll
+        for (int i = 0; i < TL_UPL; ++i)
+            if (i == li) {
+                p = (uint32_t)__builtin_amdgcn_readlane((int)upos[i], ll);
+                n = __builtin_amdgcn_readlane(ucnt[i], ll);
+                gl = __builtin_amdgcn_readlane((int)uglob[i], ll) != 0;
+            }
         Seg* dst = slab + (int64_t)p * TL_MAX_SLOTS;
         Seg hd = Seg{H, -1, -1, -1};
-        if (!__builtin_amdgcn_readlane((int)uglob, l)) {
+        if (!gl) {
             const Seg* src = lr + l * R;
             if (lane < n) {
                 hd = src[lane];
@@ -650,8 +748,9 @@ __global__ __launch_bounds__(64) void k_commit_tl(
         }
         if (lane < TL_HEAD) hdr[p].head[lane] = hd;
     }
-    if (lane < nu) hdr[upos].cnt = ucnt;
-    if (lane == 0) res[c] = CommitResult{t, stop, nu, placed};
+#pragma unroll
+    for (int i = 0; i < TL_UPL; ++i)
+        if (i * 64 + lane < nu) hdr[upos[i]].cnt = ucnt[i];
 #ifdef FIT_STAMPS
     TL_CLK(e1);
     tacc[7] += e1 - e0;
@@ -659,6 +758,167 @@ __global__ __launch_bounds__(64) void k_commit_tl(
     if (lane == 0)
         for (int i = 0; i < 12; ++i) atomicAdd(&g_tlst[c & 63][i], tacc[i]);
 #endif
+    return CommitResult{t, stop, nu, placed};
+}
+
+template <int EPL>
+__global__ __launch_bounds__(64) void k_commit_tl(
+    Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const CompPlan* __restrict__ plan,
+    const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
+    const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
+    const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
+    CommitResult* __restrict__ res, int32_t H, int32_t R) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int c = blockIdx.x;
+    const CompPlan P = plan[c];
+    const CommitResult r = commit_tl_window<EPL>(P, c, smem, slab, hdr, cand, rank_stride, nranks,
+                                                 bnd, wjob, perm, out, outs, H, R);
+    if (threadIdx.x == 0) res[c] = r;
+}
+
+// ------------------------------------------------------------------------------ k_engine_tl
+// The whole backfill placement in ONE launch, on k_engine's protocol
+// (fit_persistent.hip, fit_engine_ctl.h): blocks [0, C) are committers — one wave each runs the
+// component's rounds (publish its scan tiles to the device task ring, wait for them, commit the
+// window with commit_tl_window); blocks [C, C+W) are scan workers running scan_tile_tl.
+// Components advance at their own pace and their scans share the chip; no host round trips.
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
+    EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
+    const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
+    int ncomp, Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
+    JobRec* __restrict__ wjob, const int32_t* __restrict__ perm, int32_t* __restrict__ out,
+    int32_t* __restrict__ outs, int32_t H, int32_t slot_min, int32_t R,
+    int64_t* __restrict__ wbusy) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+
+    if ((int)blockIdx.x < ncomp) {
+        // ================================================================ committer (1 wave)
+        if (threadIdx.x >= 64) return;
+        const int c = blockIdx.x;
+        const CompState S = cs[c];
+        int32_t cursor = S.jstart, win = S.wmin;
+        unsigned target = 0;
+        int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
+        bool fail = false;
+        while (cursor < S.jend) {
+            const int w = min(win, S.jend - cursor);
+            CompPlan P;
+            P.nb = S.nb;
+            P.ne = S.ne;
+            P.sb = S.sb;
+            P.se = S.se;
+            P.nslice = S.nslice;
+            P.sub = S.sub;
+            P.jbase = cursor;
+            P.w = w;
+            P.blk0 = 0;
+            P.cand_off = S.cand_off;
+            P.slot0 = S.slot0;
+            const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            if (lane == 0) plans[c] = P;
+            for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+            release_agent();  // plan, bound reset and the last window's run lists → visible
+            const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
+            unsigned base = 0;
+            if (lane == 0)
+                base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            base = __builtin_amdgcn_readfirstlane(base);
+            for (unsigned i = lane; i < ntiles; i += 64) {
+                const unsigned idx = base + i;
+                const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
+                const unsigned long long g = ((unsigned long long)(idx / QCAP + 1) << 32) |
+                                             (tile << 10) | (sl << 6) | c;
+                __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            target += ntiles;
+            if (!wait_tiles(ctl, c, target)) {
+                fail = true;
+                break;
+            }
+            acquire_agent();  // candidates, bounds, window job rows
+            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            const CommitResult r = commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd,
+                                                       wjob, perm, out, outs, H, R);
+            const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            tw += t1 - t0;
+            tc += t2 - t1;
+            evals += (int64_t)w * (S.se - S.sb);
+            placed += r.placed;
+            ++rounds;
+            sr += r.stop == 1;
+            sd += r.stop == 2;
+            cursor += r.done;
+            const int nw = r.stop ? 2 * r.done : 2 * w;
+            win = max(S.wmin, min(S.wmax, nw));
+        }
+        if (fail && lane == 0) atomicOr(&ctl->error, 1u);
+        release_agent();  // last window's run lists / placements (kernel end also flushes)
+        if (lane == 0) {
+            co[c] = CompOut{evals, placed, cursor - S.jstart, rounds, sr, sd, tc, tw};
+            __hip_atomic_fetch_add(&ctl->finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+
+    // ======================================================================== scan worker
+    uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
+    unsigned long long* task_slot =
+        reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
+    int64_t busy = 0;  // realtime ticks (100 MHz) spent scanning
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
+            unsigned long long task = TASK_EXIT;
+            for (unsigned spins = 0;; ++spins) {
+                const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
+                                                               __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                if ((g >> 32) == want) {
+                    task = g;
+                    break;
+                }
+                if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
+                if (spins > SPIN_LIMIT) {
+                    atomicOr(&ctl->error, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            *task_slot = task;
+        }
+        __syncthreads();
+        const unsigned long long task = *task_slot;
+        if (task == TASK_EXIT) {  // block-uniform
+            if (threadIdx.x == 0) wbusy[blockIdx.x - ncomp] = busy;
+            return;
+        }
+        const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) acquire_agent();
+        else __builtin_amdgcn_s_dcache_inv();
+        __syncthreads();
+        const int c = (int)(task & 63u);
+        const int s = (int)((task >> 6) & 15u);
+        const int tile = (int)((task >> 10) & 0x3fffffu);
+        const CompPlan P = plans[c];
+        scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
+                     slot_min, xk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            release_agent();
+            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
+        }
+        __syncthreads();  // task_slot is rewritten by thread 0 next iteration
+    }
 }
 
 // Dense read-back (tests, fit_read_timeline): one block per node position, threads over slots.
@@ -749,6 +1009,47 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg*
     else if (epl <= 8) FIT_COMMIT_TL(8);
     else return hipErrorInvalidValue;
 #undef FIT_COMMIT_TL
+    return hipGetLastError();
+}
+
+// k_engine_tl: the committer takes a whole CU's LDS (run lists of up to 64 runs stay in LDS; the
+// scan workers are mostly idle at one block per CU: DESIGN.md §3.8).
+constexpr size_t TL_ENGINE_LDS = 160 * 1024;
+int engine_tl_runs(int32_t max_component_nodes) {
+    const size_t fixed = sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
+    if (fixed >= TL_ENGINE_LDS) return 0;
+    return (int)std::min<size_t>(2 * TL_PM_STEPS,
+                                 (TL_ENGINE_LDS - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP));
+}
+
+size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
+    const size_t commit = sizeof(Seg) * TL_MAX_SLOTS +
+                          (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * engine_tl_runs(max_component_nodes) +
+                          (size_t)((max_component_nodes + 31) / 32) * 4;
+    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16;
+    return std::max(commit, scan);
+}
+
+int engine_tl_blocks_per_cu(size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl, SCAN_WAVES * 64, lds) !=
+        hipSuccess)
+        return 0;
+    return n;
+}
+
+hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
+                            const void* cs, void* co, CompPlan* plans, int ncomp, Seg* slab,
+                            TlHdr* hdr, const int32_t* jl, const int32_t* jcpu,
+                            const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
+                            const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
+                            const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
+                            int32_t slot_min, int32_t R, int64_t* wbusy) {
+    hipLaunchKernelGGL(k_engine_tl, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,
+                       static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),
+                       static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,
+                       slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, perm, out,
+                       outs, H, slot_min, R, wbusy);
     return hipGetLastError();
 }
 

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfitgpu.so")
+# FITGPU_LIB: an alternative in-tree build of the same library (diagnostic / variant builds)
+LIB_PATH = os.environ.get("FITGPU_LIB") or os.path.join(_HERE, "libfitgpu.so")
 
 FIT_OK = 0
 FIT_E_INVAL = -1

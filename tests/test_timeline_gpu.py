@@ -40,20 +40,27 @@ def test_hand_case():
     check_tl(*hand_case())
 
 
+@pytest.mark.parametrize("engine", ["persistent", "rounds"])
 @pytest.mark.parametrize("nn,jj", [(64, 1024), (256, 4096), (1024, 16384), (4096, 16384)])
-def test_c5(nn, jj):
+def test_c5(nn, jj, engine, monkeypatch):
+    """persistent: one k_engine_tl launch; rounds: host-driven k_scan_tl / k_commit_tl."""
+    monkeypatch.setenv("FIT_ENGINE", engine)
     nodes, tline, jobs, parts = synth.make_c5(nn, jj)
     check_tl(nodes, tline, jobs, parts)
 
 
+@pytest.mark.parametrize("engine", ["persistent", "rounds"])
 @pytest.mark.parametrize("wmin,wmax", [(1, 1), (1, 8), (64, 64), (512, 65536)])
-def test_c5_window_policies(wmin, wmax):
+def test_c5_window_policies(wmin, wmax, engine, monkeypatch):
+    monkeypatch.setenv("FIT_ENGINE", engine)
     nodes, tline, jobs, parts = synth.make_c5(256, 4096)
     check_tl(nodes, tline, jobs, parts, window_min=wmin, window_max=wmax)
 
 
-def test_c5_full_nodes_prefix():
+@pytest.mark.parametrize("engine", ["persistent", "rounds"])
+def test_c5_full_nodes_prefix(engine, monkeypatch):
     """All 100k nodes, the first 2,000 jobs (a prefix is exact: later jobs never affect earlier)."""
+    monkeypatch.setenv("FIT_ENGINE", engine)
     nodes, tline, jobs, parts = synth.make_c5(None, 2000)
     check_tl(nodes, tline, jobs, parts)
 
