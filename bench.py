@@ -42,7 +42,7 @@ def commit_bytes_per_job(entries: int) -> int:
     return entries * 8 + 32 + 8 + 4  # candidate keys + job row + bound + placement
 
 
-def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_commit")):
+def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_commit"), engine="k_engine"):
     """Per-kernel live timings (engine HIP events) and their rooflines.
 
     Persistent engine (engine == 1): ONE k_engine launch per step; its duration is ms_device.  The
@@ -55,7 +55,7 @@ def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_comm
         ms = agg["ms_device"] / steps
         ops = evals_local / steps * SCAN_OPS_PER_EVAL
         tops = ops / (ms * 1e-3) / 1e12
-        return {"k_engine": {
+        return {engine: {
             "ms_per_launch": round(ms, 4), "launches": steps, "bound": "valu",
             "achieved": round(tops, 3), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
             "frac": round(tops / PEAK_VALU_TOPS, 4),
@@ -202,7 +202,8 @@ def main():
     if weak:
         used_mode = f"{world} independent cluster shards (one per GPU, no data-path collective)"
     kernels = kernel_table(agg, stats, a.steps, world, evals_local,
-                           ("k_scan_tl", "k_commit_tl") if tl else ("k_scan", "k_commit"))
+                           ("k_scan_tl", "k_commit_tl") if tl else ("k_scan", "k_commit"),
+                           "k_engine_tl" if tl else "k_engine")
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_launch"] * kernels[k]["launches"])
     k = kernels[dominant]
     traffic = None

@@ -132,10 +132,15 @@ __global__ __launch_bounds__(JL_BLOCK) void k_jl_count(const int8_t* __restrict_
             wm[wave][cc] = __popcll(mm);
         }
     }
-    const uint64_t rj = __ballot(k == -2), bad = __ballot(k == -3);
-    if (lane == 0 && rj) atomicAdd(&g[0], (int)__popcll(rj));
-    if (lane == 0 && bad) atomicOr(&g[1], 1);
+    __shared__ int32_t brj, bbad;
+    if (threadIdx.x == 0) brj = bbad = 0;
     __syncthreads();
+    const uint64_t rj = __ballot(k == -2), bad = __ballot(k == -3);
+    if (lane == 0 && rj) atomicAdd(&brj, (int)__popcll(rj));  // LDS; one global atomic per block
+    if (lane == 0 && bad) bbad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && brj) atomicAdd(&g[0], brj);
+    if (threadIdx.x == 0 && bbad) atomicOr(&g[1], 1);
     if ((int)threadIdx.x < ncomp) {
         int a = 0, b = 0;
         for (int w = 0; w < JL_BLOCK / 64; ++w) {

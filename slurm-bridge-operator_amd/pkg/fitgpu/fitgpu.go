@@ -120,3 +120,81 @@ func (e *Engine) PartitionFree(p int) (cpu, memMiB, gpu int64, err error) {
 	err = check(C.fit_partition_free(e.ctx, C.int32_t(p), &c, &m, &g))
 	return int64(c), int64(m), int64(g), err
 }
+
+// Releases are the end times of the jobs already running on each node (squeue EndTime), CSR by
+// node id: node x's events are [Off[x], Off[x+1]) with non-decreasing Slot (DESIGN.md §2b).
+type Releases struct {
+	Off, Slot, CPU, MemMiB, GPU []int32
+}
+
+// LoadTimeline builds the backfill horizon (slots of slotMin minutes, <= 1024 slots) on top of
+// the node table of the last LoadNodes.
+func (e *Engine) LoadTimeline(slots, slotMin int, r Releases) error {
+	if len(r.Off) == 0 {
+		return check(C.fit_load_timeline(e.ctx, C.int32_t(slots), C.int32_t(slotMin), nil, nil, nil, nil, nil))
+	}
+	var s, c, m, g *C.int32_t
+	if len(r.Slot) > 0 {
+		s, c = (*C.int32_t)(unsafe.Pointer(&r.Slot[0])), (*C.int32_t)(unsafe.Pointer(&r.CPU[0]))
+		m, g = (*C.int32_t)(unsafe.Pointer(&r.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&r.GPU[0]))
+	}
+	return check(C.fit_load_timeline(e.ctx, C.int32_t(slots), C.int32_t(slotMin),
+		(*C.int32_t)(unsafe.Pointer(&r.Off[0])), s, c, m, g))
+}
+
+// PlaceBackfill gives each job (one node) its node and earliest start slot (DESIGN.md §2b);
+// node is Unplaced when nothing fits inside the horizon, Rejected for partition limits.
+func (e *Engine) PlaceBackfill(j Jobs) (node, start []int32, st Stats, err error) {
+	cnt := len(j.CPU)
+	node, start = make([]int32, cnt), make([]int32, cnt)
+	if cnt == 0 {
+		return node, start, st, nil
+	}
+	rc := C.fit_place_tl(e.ctx, C.int32_t(cnt), (*C.int32_t)(unsafe.Pointer(&j.CPU[0])),
+		(*C.int32_t)(unsafe.Pointer(&j.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&j.GPU[0])),
+		(*C.int32_t)(unsafe.Pointer(&j.WallMin[0])), (*C.uint16_t)(unsafe.Pointer(&j.Part[0])),
+		(*C.int32_t)(unsafe.Pointer(&node[0])), (*C.int32_t)(unsafe.Pointer(&start[0])), &st)
+	return node, start, st, check(rc)
+}
+
+// IngestNodes turns `scontrol show nodes` output into the engine's node table (Client.Nodes +
+// parseNode, pkg/slurm-agent/slurm.go:354-363 / parse.go:291-308, plus Gres/GresUsed, State,
+// Partitions and NodeName), partitions[p] = the partition of part_mask bit p.
+func IngestNodes(text string, partitions []string) (Nodes, []string, error) {
+	ct := C.CString(text)
+	defer C.free(unsafe.Pointer(ct))
+	blob := make([]byte, 0, 64)
+	for _, p := range partitions {
+		blob = append(append(blob, p...), 0)
+	}
+	blob = append(blob, 0)
+	cp := C.CBytes(blob)
+	defer C.free(cp)
+	capn := 2
+	for i := 0; i+1 < len(text); i++ {
+		if text[i] == '\n' && text[i+1] == '\n' {
+			capn++
+		}
+	}
+	n := Nodes{make([]int32, capn), make([]int32, capn), make([]int32, capn), make([]int32, capn),
+		make([]uint32, capn)}
+	names := make([]byte, len(text)+64)
+	rc := C.fit_ingest_nodes(ct, (*C.char)(cp), C.int32_t(len(partitions)), C.int32_t(capn),
+		(*C.int32_t)(unsafe.Pointer(&n.CPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.MemFreeMiB[0])),
+		(*C.int32_t)(unsafe.Pointer(&n.GPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.AvailMin[0])),
+		(*C.uint32_t)(unsafe.Pointer(&n.PartMask[0])), (*C.char)(unsafe.Pointer(&names[0])),
+		C.int32_t(len(names)))
+	if err := check(rc); err != nil {
+		return Nodes{}, nil, err
+	}
+	cnt := int(rc)
+	n = Nodes{n.CPUFree[:cnt], n.MemFreeMiB[:cnt], n.GPUFree[:cnt], n.AvailMin[:cnt], n.PartMask[:cnt]}
+	out := make([]string, 0, cnt)
+	for i, b := 0, 0; i < len(names) && len(out) < cnt; i++ {
+		if names[i] == 0 {
+			out = append(out, string(names[b:i]))
+			b = i + 1
+		}
+	}
+	return n, out, nil
+}
