@@ -24,8 +24,21 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
     from fitgpu import Engine, TorchHostExchange, synth
-    nodes, jobs, parts = synth.make_config(a.config, a.nodes, a.jobs)
     x = TorchHostExchange()
+    if a.config == "c5":  # backfill: node-sharded rounds over replicated run lists
+        nodes, tline, jobs, parts = synth.make_c5(a.nodes, a.jobs)
+        with Engine(device=0, rank=a.rank, world=a.world, exchange=x, shard_mode=a.mode) as e:
+            e.load_nodes(nodes)
+            e.load_partitions(parts)
+            e.load_timeline(tline)
+            node, start, st = e.place_tl(jobs)
+            fin = e.read_timeline()
+        np.savez(a.out, node=node, start=start, fin=fin,
+                 stats=np.array([st["placed"], st["unplaced"], st["rejected"], st["shard_mode"]]))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    nodes, jobs, parts = synth.make_config(a.config, a.nodes, a.jobs)
     with Engine(device=0, rank=a.rank, world=a.world, exchange=x, shard_mode=a.mode) as e:
         e.load_nodes(nodes)
         e.load_partitions(parts)

@@ -1,0 +1,43 @@
+"""bench.py keeps the driver's contract: one JSON line with the required keys, the roofline and
+CPU-baseline objects, for the C3 headline and the C5 workload; N>1 weak scaling rehearsed with two
+ranks on one GPU (gloo for the timing collectives)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def run(args, env=None, timeout=240):
+    r = subprocess.run([sys.executable, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env={**os.environ, **(env or {})})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("workload", ["c3", "c5"])
+def test_bench_line(workload):
+    d = run(["bench.py", "--workload", workload, "--steps", "1", "--warmup", "1", "--cpu-sample", "200"])
+    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
+    assert set(d["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    assert d["config"]["workload"] == workload and d["config"]["jobs"] == 1_000_000
+
+
+def test_bench_two_rank_rehearsal():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    d = run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+             "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse"])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["jobs"] == 2_000_000 and d["config"]["per_gpu"]["jobs"] == 1_000_000

@@ -43,3 +43,26 @@ def test_two_ranks_match_oracle(tmp_path, mode, config, nn, jj):
             assert np.array_equal(d[k], col)
         assert list(d["stats"][:3]) == [rst["placed"], rst["unplaced"], rst["rejected"]]
         assert d["stats"][3] == mode
+
+
+def test_two_ranks_backfill_match_oracle(tmp_path):
+    """C5 (SPEC §2b) node-sharded over 2 ranks: each scans half of every component, candidates and
+    bounds are exchanged every round, the commit runs replicated; both ranks equal the oracle."""
+    port = free_port()
+    nn, jj = 2048, 16384
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_multirank_worker.py"), "--rank", str(r),
+                               "--world", "2", "--port", str(port), "--mode", str(FIT_SHARD_NODES),
+                               "--config", "c5", "--nodes", str(nn), "--jobs", str(jj),
+                               "--out", str(tmp_path / f"r{r}.npz")])
+             for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    nodes, tline, jobs, parts = synth.make_c5(nn, jj)
+    rn, rs, rst, rfin = po.ref_place_tl(nodes, tline, jobs, parts)
+    live = nodes.part_mask != 0
+    for r in range(2):
+        d = np.load(tmp_path / f"r{r}.npz")
+        assert np.array_equal(d["node"], rn) and np.array_equal(d["start"], rs)
+        assert np.array_equal(d["fin"][live], rfin[live])
+        assert list(d["stats"][:3]) == [rst["placed"], rst["unplaced"], rst["rejected"]]
+        assert d["stats"][3] == FIT_SHARD_NODES
