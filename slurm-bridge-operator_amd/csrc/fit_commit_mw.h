@@ -114,12 +114,53 @@ struct MwTiles {
     unsigned need;          // nslice
 };
 
-__device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
+// global address-space views of the helper's buffers: a plain (generic) pointer in a non-inlined
+// function compiles to flat loads, which also count in lgkmcnt — every LDS wait would then drain
+// the prefetched job stream
+#define GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ const GAS T* gview(const T* p) {
+    return (const GAS T*)p;
+}
+
+typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ NodeRec ld_node(const GAS NodeRec* p) {
+    const GAS v4i32* q = (const GAS v4i32*)p;
+    const v4i32 a = q[0], b = q[1];
+    NodeRec r;
+    r.cpu = a.x;
+    r.mem = a.y;
+    r.gpu = a.z;
+    r.avail = a.w;
+    r.mask = (uint32_t)b.x;
+    r.orig = b.y;
+    r.pad0 = b.z;
+    r.pad1 = b.w;
+    return r;
+}
+
+__device__ __forceinline__ JobRec ld_job(const GAS JobRec* p) {
+    const GAS v4i32* q = (const GAS v4i32*)p;
+    const v4i32 a = q[0], b = q[1];
+    JobRec r;
+    r.q = a.x;
+    r.cpu = a.y;
+    r.mem = a.z;
+    r.gpu = a.w;
+    r.wall = b.x;
+    r.pbit = (uint32_t)b.y;
+    r.k = b.z;
+    r.pad = b.w;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t ld_agent_u64(const GAS uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ JobRec ld_agent_job(const JobRec* p) {
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+__device__ __forceinline__ JobRec ld_agent_job(const GAS JobRec* p) {
+    const GAS uint64_t* q = (const GAS uint64_t*)p;
     const uint64_t a = ld_agent_u64(q), b = ld_agent_u64(q + 1), c = ld_agent_u64(q + 2),
                    d = ld_agent_u64(q + 3);
     JobRec r;
@@ -159,7 +200,8 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
     const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
     if (tile < ready) return true;
     for (unsigned sp = 0;; ++sp) {
-        if (__hip_atomic_load(T.tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= T.need)
+        if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+            T.need)
             break;
         if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
         if (sp > MW_SPIN_LIMIT) {
@@ -182,7 +224,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         { /* node rows of job t+H's candidates (keys arrived last step) */                     \
             const uint64_t k_ = kk[B_];                                                        \
             const uint32_t p_ = k_ != KEY_INF ? (uint32_t)k_ : (uint32_t)P.nb;                 \
-            const NodeRec r_ = rec[p_];                                                        \
+            const NodeRec r_ = ld_node(rec + p_);                                              \
             rc[B_] = r_.cpu;                                                                   \
             rm[B_] = r_.mem;                                                                   \
             rg[B_] = r_.gpu;                                                                   \
@@ -199,7 +241,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
                 jbd[C] = ld_agent_u64(bnd + P.slot0 + tt_);                                    \
             } else {                                                                           \
                 kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                         \
-                jr[C] = wjob[P.slot0 + tt_];                                                   \
+                jr[C] = ld_job(wjob + P.slot0 + tt_);                                          \
                 jbd[C] = bnd[P.slot0 + tt_];                                                   \
             }                                                                                  \
         }                                                                                      \
@@ -287,11 +329,18 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         t += MW_H;                                                                             \
     }
 
-__device__ __noinline__ void mw_helper(const CompPlan& P, MwShared* S,
-                                          const NodeRec* __restrict__ rec,
-                                          const uint64_t* __restrict__ cand,
-                                          const uint64_t* __restrict__ bnd,
-                                          const JobRec* __restrict__ wjob, int h, MwTiles T) {
+__device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* S,
+                                          const NodeRec* __restrict__ rec_,
+                                          const uint64_t* __restrict__ cand_,
+                                          const uint64_t* __restrict__ bnd_,
+                                          const JobRec* __restrict__ wjob_, int h, MwTiles T) {
+    const GAS NodeRec* const rec = gview(rec_);
+    const GAS uint64_t* const cand = gview(cand_);
+    const GAS uint64_t* const bnd = gview(bnd_);
+    const GAS JobRec* const wjob = gview(wjob_);
+    // by value: a reference into the caller's stack is re-read (flat load + full vmcnt wait) after
+    // every LDS store, which would drain the job-stream prefetch each step
+    const CompPlan P = Pref;
     const int lane = threadIdx.x & 63;
     const int E = P.nslice * KS;
     const bool has = lane < E;
@@ -315,13 +364,13 @@ __device__ __noinline__ void mw_helper(const CompPlan& P, MwShared* S,
             jbd[s] = ld_agent_u64(bnd + P.slot0 + tt);
         } else {
             kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
-            jr[s] = wjob[P.slot0 + tt];
+            jr[s] = ld_job(wjob + P.slot0 + tt);
             jbd[s] = bnd[P.slot0 + tt];
         }
     }
     {
         const uint32_t p = kk[0] != KEY_INF ? (uint32_t)kk[0] : (uint32_t)P.nb;
-        const NodeRec r = rec[p];
+        const NodeRec r = ld_node(rec + p);
         rc[0] = r.cpu;
         rm[0] = r.mem;
         rg[0] = r.gpu;
@@ -391,8 +440,9 @@ __device__ __forceinline__ uint64_t any_in_byte(uint64_t m) {
 
 // Out of line (as is mw_helper): called once per round, each gets its own register allocation
 // instead of sharing the persistent kernel's (which otherwise spills SGPRs in this loop).
-__device__ __noinline__ CommitResult mw_decider(const CompPlan& P, MwShared* S,
+__device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* S,
                                                 int32_t* __restrict__ out, int kmax) {
+    const CompPlan P = Pref;  // by value (see mw_helper)
     const int lane = threadIdx.x & 63;
     const int r8 = lane & 7;   // ring entry this lane holds (full row in lanes 0..7 only)
     const int i8 = lane >> 3;  // record item this lane reads: lane 8i + r tests item i vs entry r

@@ -24,7 +24,7 @@ namespace fitgpu {
 
 // Windows holding a multi-node job: the single-wave commit (fit_common.h), kept out of line so
 // its registers are allocated apart from the decider / helper / worker loops.
-__device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan& P, NodeRec* rec,
+__device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan P, NodeRec* rec,
                                                           const uint64_t* cand,
                                                           const uint64_t* bnd, const JobRec* wjob,
                                                           int32_t* out, int kmax,
