@@ -472,7 +472,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
     TlHdr* __restrict__ hdr, const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
     const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
     const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
-    int32_t H, int32_t R) {
+    int32_t H, int32_t R, const unsigned* tdone = nullptr, unsigned need = 0) {
     Seg* scr = reinterpret_cast<Seg*>(smem);                // general-path scratch
     Seg* lr = scr + TL_MAX_SLOTS;                           // TL_UCAP regions of R runs
     int4* pmr = reinterpret_cast<int4*>(lr + TL_UCAP * R);  // their prefix minima
@@ -517,11 +517,33 @@ __device__ __forceinline__ CommitResult commit_tl_window(
 #ifdef FIT_STAMPS
     unsigned long long tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    JobRec J = wjob[P.slot0 + z];
-    uint64_t B = bnd[P.slot0 + z];
+    // tdone (k_engine_tl): the window is committed while its scan tiles run; before a job's row,
+    // bound and candidates are read, its tile must have all `need` slices done; an agent-scope
+    // acquire when a tile turns ready drops this CU's L1 (the buffers are reused every round and
+    // may be cached stale), so the reads themselves stay plain, prefetchable loads
+    int ready = 0;
+    bool tfail = false;
+    auto tile_ready = [&](int tt) {
+        if (!tdone) return true;
+        const int tile = tt / SCAN_JOBS;
+        if (tile < ready) return true;
+        for (unsigned sp = 0;; ++sp) {
+            if (__hip_atomic_load(tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+            if (sp > SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        ready = tile + 1;
+        return true;
+    };
+    auto ld64 = [&](const uint64_t* p) { return *p; };
+    auto ldjob = [&](const JobRec* p) { return *p; };
+    if (!tile_ready(0)) return CommitResult{0, 3, 0, 0};
+    JobRec J = ldjob(wjob + P.slot0 + z);
+    uint64_t B = ld64(bnd + P.slot0 + z);
     uint64_t kr[EPL];
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) kr[k] = cand[off[k]];
+    for (int k = 0; k < EPL; ++k) kr[k] = ld64(cand + off[k]);
     for (; t < P.w; ++t) {
         TL_CLK(c0);
         uint64_t cm = KEY_INF;
@@ -544,12 +566,22 @@ __device__ __forceinline__ CommitResult commit_tl_window(
             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)B);
         {  // the next job's stream, in flight during this one
             const int tn = min(t + 1, P.w - 1);
-            J = wjob[P.slot0 + tn + z];
-            B = bnd[P.slot0 + tn + z];
+            if (!tile_ready(tn)) {
+                tfail = true;
+                break;
+            }
+            J = ldjob(wjob + P.slot0 + tn + z);
+            B = ld64(bnd + P.slot0 + tn + z);
 #pragma unroll
-            for (int k = 0; k < EPL; ++k) kr[k] = cand[off[k] + (int64_t)tn * per_rank];
+            for (int k = 0; k < EPL; ++k) kr[k] = ld64(cand + off[k] + (int64_t)tn * per_rank);
         }
         const uint64_t cw = wave_min_key(cm);
+        // a clean node can only win as cw: fetch its header, first 64 runs and id now, so a new
+        // dirty node costs no memory round trip when the decision comes
+        const uint32_t cpos = cw != KEY_INF ? ((uint32_t)cw & TL_POS_MASK) : (uint32_t)P.nb;
+        const TlHdr ch = hdr[cpos + z];
+        const Seg crun = slab[(int64_t)cpos * TL_MAX_SLOTS + lane];
+        const int32_t corig = perm[cpos + z];
         TL_CLK(c1);
         TL_ACC(0, c0, c1);
         // LDS lists: a start at slot 0 through the prefix minima — k = the first run ending at or
@@ -630,16 +662,16 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                     break;
                 }
                 l = nu++;
-                const TlHdr h0 = hdr[pos + z];
+                // pos == cpos: the winner is the clean best (prefetched above)
+                const TlHdr& h0 = ch;
                 const int n0 = __builtin_amdgcn_readfirstlane(h0.cnt);
                 const bool g = n0 > R;
                 if (!g) {
-                    const Seg* src = slab + (int64_t)pos * TL_MAX_SLOTS;
                     Seg* dst = lr + l * R;
-                    if (lane < n0) dst[lane] = src[lane];  // n0 <= R <= 64
+                    if (lane < n0) dst[lane] = crun;  // n0 <= R <= 64
                     tl_pm_build(dst, pmr + l * R, n0);
                 }
-                const int32_t o0 = perm[pos];
+                const int32_t o0 = corig;
 #pragma unroll
                 for (int i = 0; i < TL_UPL; ++i)
                     if (i * 64 + lane == l) {
@@ -758,6 +790,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
     if (lane == 0)
         for (int i = 0; i < 12; ++i) atomicAdd(&g_tlst[c & 63][i], tacc[i]);
 #endif
+    if (tfail) stop = 3;  // watchdog: a scan tile never completed
     return CommitResult{t, stop, nu, placed};
 }
 
@@ -819,10 +852,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             P.cand_off = S.cand_off;
             P.slot0 = S.slot0;
             const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            // the previous window's tiles (also those past its stop) must all be complete before
+            // their buffers and counters are reused
+            if (!wait_tiles(ctl, c, target)) {
+                fail = true;
+                break;
+            }
+            const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
             if (lane == 0) plans[c] = P;
             for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
-            release_agent();  // plan, bound reset and the last window's run lists → visible
-            const unsigned ntiles = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS * S.nslice);
+            for (unsigned i = lane; i < ntj; i += 64)
+                __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            release_agent();  // plan, bound / counter reset and the last window's run lists
+            const unsigned ntiles = ntj * (unsigned)S.nslice;
             unsigned base = 0;
             if (lane == 0)
                 base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
@@ -837,14 +879,15 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
             target += ntiles;
-            if (!wait_tiles(ctl, c, target)) {
+            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            // committed while its tiles are scanned: per-tile readiness inside
+            const CommitResult r = commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd,
+                                                       wjob, perm, out, outs, H, R,
+                                                       &ctl->tdone[c][0], (unsigned)S.nslice);
+            if (r.stop == 3) {
                 fail = true;
                 break;
             }
-            acquire_agent();  // candidates, bounds, window job rows
-            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            const CommitResult r = commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd,
-                                                       wjob, perm, out, outs, H, R);
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
             tw += t1 - t0;
             tc += t2 - t1;
@@ -914,6 +957,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         __syncthreads();
         if (threadIdx.x == 0) {
             release_agent();
+            __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
