@@ -183,6 +183,38 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
+// A dynamic-LDS pointer the compiler cannot re-derive: in an out-of-line function the constant
+// shared base is otherwise rematerialised from the dynlds offset table (an s_load + lgkmcnt(0)
+// wait) on every loop iteration; laundered through an SGPR it is computed once.  The round trip
+// through address space 3 keeps every access a ds_* instruction.
+template <class T>
+__device__ __forceinline__ T* lds_opaque(T* p) {
+    uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+    asm volatile("" : "+s"(a));
+    return (T*)(__attribute__((address_space(3))) T*)(uintptr_t)a;
+}
+
+// The plan copied into SGPRs: an out-of-line function receives it through a generic pointer, and
+// fields loaded that way sit in VGPRs, so the compiler cannot prove the job loop uniform (it
+// would run it under exec masks with its counter in a VGPR).
+__device__ __forceinline__ int32_t rfl(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ CompPlan plan_sgpr(const CompPlan& q) {
+    CompPlan p;
+    p.nb = rfl(q.nb);
+    p.ne = rfl(q.ne);
+    p.sb = rfl(q.sb);
+    p.se = rfl(q.se);
+    p.nslice = rfl(q.nslice);
+    p.sub = rfl(q.sub);
+    p.jbase = rfl(q.jbase);
+    p.w = rfl(q.w);
+    p.blk0 = rfl(q.blk0);
+    p.cand_off = (int64_t)(((uint64_t)(uint32_t)rfl((int32_t)(q.cand_off >> 32)) << 32) |
+                           (uint32_t)rfl((int32_t)q.cand_off));
+    p.slot0 = rfl(q.slot0);
+    return p;
+}
+
 __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, int32_t av,
                                            uint32_t mask, uint32_t pos, int32_t jc, int32_t jm,
                                            int32_t jg, int32_t jw, uint32_t jp) {
@@ -329,7 +361,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         t += MW_H;                                                                             \
     }
 
-__device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* S,
+__device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
                                           const NodeRec* __restrict__ rec_,
                                           const uint64_t* __restrict__ cand_,
                                           const uint64_t* __restrict__ bnd_,
@@ -340,7 +372,8 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* S,
     const GAS JobRec* const wjob = gview(wjob_);
     // by value: a reference into the caller's stack is re-read (flat load + full vmcnt wait) after
     // every LDS store, which would drain the job-stream prefetch each step
-    const CompPlan P = Pref;
+    const CompPlan P = plan_sgpr(Pref);
+    MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
     const int E = P.nslice * KS;
     const bool has = lane < E;
@@ -440,9 +473,10 @@ __device__ __forceinline__ uint64_t any_in_byte(uint64_t m) {
 
 // Out of line (as is mw_helper): called once per round, each gets its own register allocation
 // instead of sharing the persistent kernel's (which otherwise spills SGPRs in this loop).
-__device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* S,
+__device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* Sin,
                                                 int32_t* __restrict__ out, int kmax) {
-    const CompPlan P = Pref;  // by value (see mw_helper)
+    const CompPlan P = plan_sgpr(Pref);  // by value (see mw_helper)
+    MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
     const int r8 = lane & 7;   // ring entry this lane holds (full row in lanes 0..7 only)
     const int i8 = lane >> 3;  // record item this lane reads: lane 8i + r tests item i vs entry r
@@ -478,8 +512,8 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
 #ifdef MW_DECIDER_BENCH
             if (true) break;  // diagnostic: records pre-filled, no helpers
 #endif
-            if (__builtin_amdgcn_readfirstlane(h.ready) == (uint32_t)t + 1u) break;
-            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
+            if ((uint32_t)__builtin_amdgcn_readfirstlane(h.ready) == (uint32_t)t + 1u) break;
+            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {  // uniform exit
                 lds_st(&S->fail, 1u);
                 stop = 3;
                 break;
@@ -581,7 +615,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
         oq = writelane(__builtin_amdgcn_readfirstlane(h.q), t & 63, oq);
         ov = writelane(node, t & 63, ov);
         if ((t & 63) == 63) {  // uniform: flush 64 placements
-            if (oq >= 0) out[(int64_t)oq * kmax] = ov;
+            if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // global: vmcnt only
             oq = -1;
         }
         cbar();
@@ -592,7 +626,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
         MW_CLK(dw3);
         MW_ACC(a_dd, dw3 - dw2);
     }
-    if (oq >= 0 && lane < (t & 63)) out[(int64_t)oq * kmax] = ov;  // last partial group
+    if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
     if (stop) lds_st(&S->halt, 1u);
     MW_CLK(d1);
     MW_ADD(0, d1 - d0);
