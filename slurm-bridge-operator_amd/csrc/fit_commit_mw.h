@@ -106,9 +106,9 @@ __device__ __forceinline__ void cbar() { __builtin_amdgcn_fence(__ATOMIC_RELEASE
 
 // Tile readiness: the window's scan tiles complete while the window is being
 // committed; a helper waits for the (job tile)'s per-tile counter to reach nslice before reading
-// that tile's candidates, bound and job row — with agent-scope (L1-bypassing) loads, since the
-// committer's CU may hold stale lines of these reused buffers.  tdone == nullptr: the whole
-// window was acquired before the commit (no waits).
+// that tile's candidates, bound and job row; an agent-scope acquire when a tile turns ready drops
+// the CU's L1 (it may hold stale lines of these reused buffers), so the reads stay plain loads.
+// tdone == nullptr: the whole window was acquired before the commit (no waits).
 struct MwTiles {
     const unsigned* tdone;  // per-tile completed slice counts of this component's window
     unsigned need;          // nslice
@@ -152,26 +152,6 @@ __device__ __forceinline__ JobRec ld_job(const GAS JobRec* p) {
     r.pbit = (uint32_t)b.y;
     r.k = b.z;
     r.pad = b.w;
-    return r;
-}
-
-__device__ __forceinline__ uint64_t ld_agent_u64(const GAS uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ JobRec ld_agent_job(const GAS JobRec* p) {
-    const GAS uint64_t* q = (const GAS uint64_t*)p;
-    const uint64_t a = ld_agent_u64(q), b = ld_agent_u64(q + 1), c = ld_agent_u64(q + 2),
-                   d = ld_agent_u64(q + 3);
-    JobRec r;
-    r.q = (int32_t)(uint32_t)a;
-    r.cpu = (int32_t)(a >> 32);
-    r.mem = (int32_t)(uint32_t)b;
-    r.gpu = (int32_t)(b >> 32);
-    r.wall = (int32_t)(uint32_t)c;
-    r.pbit = (uint32_t)(c >> 32);
-    r.k = (int32_t)(uint32_t)d;
-    r.pad = (int32_t)(d >> 32);
     return r;
 }
 
@@ -242,6 +222,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         }
         __builtin_amdgcn_s_sleep(1);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ready = tile + 1;
     return true;
 }
@@ -267,15 +248,9 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         {                                                                                      \
             const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
             if (!mw_tile_ready(T, tt_, ready, S)) goto hdone;                                  \
-            if (T.tdone) {                                                                     \
-                kk[C] = has ? ld_agent_u64(cand + eoff + (int64_t)tt_ * E) : KEY_INF;          \
-                jr[C] = ld_agent_job(wjob + P.slot0 + tt_);                                    \
-                jbd[C] = ld_agent_u64(bnd + P.slot0 + tt_);                                    \
-            } else {                                                                           \
-                kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                         \
-                jr[C] = ld_job(wjob + P.slot0 + tt_);                                          \
-                jbd[C] = bnd[P.slot0 + tt_];                                                   \
-            }                                                                                  \
+            kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                             \
+            jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
+            jbd[C] = bnd[P.slot0 + tt_];                                                       \
         }                                                                                      \
         /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs */                  \
         uint32_t v_;                                                                           \
@@ -290,7 +265,8 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
             }                                                                                  \
             __builtin_amdgcn_s_sleep(MW_HSLEEP); /* keep the LDS free for the decider */       \
         }                                                                                      \
-        cbar();                                                                                \
+        /* the snapshot's row / bitmap reads are issued after the flag read that admitted it */ \
+        asm volatile("" ::: "memory");                                                         \
         {                                                                                      \
             MW_CLK(hw1_);                                                                      \
             MW_ACC(a_hw, hw1_ - hw0_);                                                         \
@@ -391,15 +367,9 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     for (int s = 0; s < 2; ++s) {  // jobs t and t + H
         const int tt = min(t + s * MW_H, wlast) + z;
         if (!mw_tile_ready(T, tt, ready, S)) return;  // halted / watchdog
-        if (T.tdone) {
-            kk[s] = has ? ld_agent_u64(cand + eoff + (int64_t)tt * E) : KEY_INF;
-            jr[s] = ld_agent_job(wjob + P.slot0 + tt);
-            jbd[s] = ld_agent_u64(bnd + P.slot0 + tt);
-        } else {
-            kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
-            jr[s] = ld_job(wjob + P.slot0 + tt);
-            jbd[s] = bnd[P.slot0 + tt];
-        }
+        kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
+        jr[s] = ld_job(wjob + P.slot0 + tt);
+        jbd[s] = bnd[P.slot0 + tt];
     }
     {
         const uint32_t p = kk[0] != KEY_INF ? (uint32_t)kk[0] : (uint32_t)P.nb;
@@ -456,7 +426,10 @@ __device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
 // select goes through M0 (one SGPR operand per VALU instruction on gfx9).
 __device__ __forceinline__ int32_t writelane(int32_t x, int l, int32_t old) {
     int32_t r;
-    asm("v_writelane_b32 %0, %1, m0" : "=v"(r) : "s"(x), "{m0}"(l), "0"(old));
+    // readfirstlane: a value the compiler believes divergent would otherwise get a VGPR here
+    asm("v_writelane_b32 %0, %1, m0"
+        : "=v"(r)
+        : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(l), "0"(old));
     return r;
 }
 __device__ __forceinline__ uint32_t writelane(uint32_t x, int l, uint32_t old) {
@@ -469,6 +442,23 @@ __device__ __forceinline__ uint64_t any_in_byte(uint64_t m) {
     m |= m >> 2;
     m |= m >> 1;
     return m & 0x0101010101010101ull;
+}
+
+// one lane's view of a record: the header (every lane) and item i8 (lanes 8 i8 + r)
+__device__ __forceinline__ void mw_read_rec(const MwRec* R, int i8, uint4& h0, uint4& h1,
+                                            uint4& h2, uint4& i0, uint4& i1, uint4& i2) {
+    // {ready, v, n, q} is one 16-byte LDS store on the helper side (its last); read first
+    const uint4* hp = reinterpret_cast<const uint4*>(&R->h);
+    const uint4* ip = reinterpret_cast<const uint4*>(&R->it[i8]);
+    h0 = hp[0];
+    // plain LDS loads may be issued in any order: keep the flag word's read first (the wave's
+    // DS instructions then execute in issue order, after the helper's record stores it saw)
+    asm volatile("" ::: "memory");
+    h1 = hp[1];
+    h2 = hp[2];
+    i0 = ip[0];
+    i1 = ip[1];
+    i2 = ip[2];
 }
 
 // Out of line (as is mw_helper): called once per round, each gets its own register allocation
@@ -493,26 +483,14 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MW_DECL(a_dd);
     MW_CLK(d0);
     for (; t < P.w; ++t) {
-        MwRec* R = &S->rec[t & (MW_R - 1)];
         MW_CLK(dw0);
-        MwHdr h;
-        MwItem it;
+        uint4 h0, h1, h2, i0, i1, i2;
         for (unsigned sp = 0;; ++sp) {  // speculative: header and items in one round trip
-            // {ready, v, n, q} is one 16-byte LDS store on the helper side (its last); read as one
-            const uint4* hp = reinterpret_cast<const uint4*>(&R->h);
-            const uint4* ip = reinterpret_cast<const uint4*>(&R->it[i8]);
-            const uint4 h0 = hp[0], h1 = hp[1], h2 = hp[2];
-            const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2];
-            h = MwHdr{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
-                      (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
-                      ((uint64_t)h2.w << 32) | h2.z};
-            it = MwItem{((uint64_t)i0.y << 32) | i0.x, (int32_t)i0.z, (int32_t)i0.w,
-                        (int32_t)i1.x, (int32_t)i1.y, (int32_t)i1.z, (int32_t)i1.w,
-                        i2.x, i2.y, i2.z, i2.w};
+            mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
 #ifdef MW_DECIDER_BENCH
             if (true) break;  // diagnostic: records pre-filled, no helpers
 #endif
-            if ((uint32_t)__builtin_amdgcn_readfirstlane(h.ready) == (uint32_t)t + 1u) break;
+            if ((uint32_t)rfl((int32_t)h0.x) == (uint32_t)t + 1u) break;
             if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {  // uniform exit
                 lds_st(&S->fail, 1u);
                 stop = 3;
@@ -520,6 +498,12 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
             }
             __builtin_amdgcn_s_sleep(0);
         }
+        const MwHdr h{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
+                      (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
+                      ((uint64_t)h2.w << 32) | h2.z};
+        const MwItem it{((uint64_t)i0.y << 32) | i0.x, (int32_t)i0.z, (int32_t)i0.w,
+                        (int32_t)i1.x, (int32_t)i1.y, (int32_t)i1.z, (int32_t)i1.w,
+                        i2.x, i2.y, i2.z, i2.w};
         if (stop) break;
         MW_CLK(dw1);
         MW_ACC(a_dw, dw1 - dw0);

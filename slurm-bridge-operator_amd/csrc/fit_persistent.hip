@@ -206,7 +206,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         if (threadIdx.x == 0) {
             release_agent();
             __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the tile count must land before the done count: once a committer sees `done` reach
+            // its target it resets the tile counters for the next round, and a late increment
+            // would then mark a tile of that round complete before it was scanned
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();  // task_slot is rewritten by thread 0 next iteration
