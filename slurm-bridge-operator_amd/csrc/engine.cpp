@@ -443,7 +443,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // the serial commit chain (measured: 2/CU → commit +3%, no scan gain).
     int workers = std::max(8, std::max(1, per_cu - 1) * c->cus - nc);
     if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
-    if (c->ebusy.ensure(workers) || c->h_ebusy.ensure(workers)) return FIT_E_OOM;
+    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers)) return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
@@ -453,7 +453,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
                           c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p, c->jpk.p));
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * workers,
+    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
                            hipMemcpyDeviceToHost, st));
     // error word: EngineCtl::error sits at byte offset 2 * 128 + 4
     HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
@@ -463,7 +463,12 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device += ms;
     int64_t busy = 0;
-    for (int i = 0; i < workers; ++i) busy += c->h_ebusy.p[i];
+    // per worker {busy ticks, evaluations scanned}: tiles of a finished round are dropped, so
+    // the performed evaluations are counted where they happen
+    for (int i = 0; i < workers; ++i) {
+        busy += c->h_ebusy.p[2 * i];
+        S.evals += c->h_ebusy.p[2 * i + 1];
+    }
     S.ms_scan += busy / 1e5 / workers;  // average worker busy time (100 MHz ticks)
     double commit_max = 0;
     for (int i = 0; i < nc; ++i) {
@@ -472,7 +477,6 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         if (o.done_jobs != jb[k + 1] - jb[k])
             return fail(FIT_E_HIP, "component %d resolved %lld of %d jobs", k, (long long)o.done_jobs,
                         jb[k + 1] - jb[k]);
-        S.evals += o.evals;
         S.placed += o.placed;
         S.rounds = std::max<int64_t>(S.rounds, o.rounds);
         S.stops_rescan += o.stops_rescan;
@@ -725,7 +729,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine_tl does not fit on a CU (lds %zu)", lds);
     int workers = std::max(8, per_cu * c->cus - nc);
     if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
-    if (c->ebusy.ensure(workers) || c->h_ebusy.ensure(workers)) return FIT_E_OOM;
+    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers)) return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
@@ -736,7 +740,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
                              c->tl_slots, c->tl_slot_min, R, c->ebusy.p));
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * workers,
+    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -745,7 +749,12 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device += ms;
     int64_t busy = 0;
-    for (int i = 0; i < workers; ++i) busy += c->h_ebusy.p[i];
+    // per worker {busy ticks, evaluations scanned}: tiles of a finished round are dropped, so
+    // the performed evaluations are counted where they happen
+    for (int i = 0; i < workers; ++i) {
+        busy += c->h_ebusy.p[2 * i];
+        S.evals += c->h_ebusy.p[2 * i + 1];
+    }
     S.ms_scan += busy / 1e5 / workers;
     double commit_max = 0;
     for (int i = 0; i < nc; ++i) {
@@ -754,7 +763,6 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         if (o.done_jobs != jb[k + 1] - jb[k])
             return fail(FIT_E_HIP, "component %d resolved %lld of %d jobs", k, (long long)o.done_jobs,
                         jb[k + 1] - jb[k]);
-        S.evals += o.evals;
         S.placed += o.placed;
         S.rounds = std::max<int64_t>(S.rounds, o.rounds);
         S.stops_rescan += o.stops_rescan;

@@ -83,7 +83,7 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 #ifdef FIT_STAMPS
 // [comp][0] decider cycles, [1] decider wait-for-record, [2] decided jobs,
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
-// [7] decider check+reduce, [8] decider decide+publish
+// [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs
 __device__ unsigned long long g_mw[64][16];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define MW_DECL(v) unsigned long long v = 0
@@ -479,6 +479,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     uint32_t wk = 0, wp = ~0u;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
     MW_DECL(a_dw);
+    MW_DECL(a_d0);  // waits of the round's first MW_R jobs (pipeline fill)
     MW_DECL(a_dc);
     MW_DECL(a_dd);
     MW_CLK(d0);
@@ -507,6 +508,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
         if (stop) break;
         MW_CLK(dw1);
         MW_ACC(a_dw, dw1 - dw0);
+        MW_ACC(a_d0, t < MW_R ? dw1 - dw0 : 0);
         const int v = __builtin_amdgcn_readfirstlane(h.v);
         const int n = __builtin_amdgcn_readfirstlane(h.n);
         const bool live = wj >= v;
@@ -616,6 +618,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MW_ADD(0, d1 - d0);
     MW_ADD(2, t);
     MW_ADD(1, a_dw);
+    MW_ADD(9, a_d0);
     MW_ADD(7, a_dc);
     MW_ADD(8, a_dd);
     return CommitResult{t, stop, nu, placed};

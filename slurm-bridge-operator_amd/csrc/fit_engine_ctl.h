@@ -21,10 +21,35 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned pad2[30];
     unsigned done[32][32];  // per component tiles completed (own 128-B line each)
     unsigned tdone[32][ENGINE_TILES];  // per component, per window job tile: slices completed
+    unsigned long long pub[32];        // FIT_STAMPS: realtime of each component's last publish
 };
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Task word: {epoch:32 | skip:1 | round:14 | tile:7 | slice:4 | component:6}.  done[c][1] holds
+// the round tag of component c's last finished commit: a task of that round is dropped unscanned
+// (it only counts as done) — a round that stops early leaves its later tiles unneeded, and
+// scanning them would delay both the next round's start and other components' tiles.
+static_assert(ENGINE_TILES <= 128, "7 tile bits");
+constexpr unsigned long long TASK_SKIP = 1ull << 31;
+__device__ __forceinline__ unsigned long long engine_task(unsigned long long epoch, unsigned round,
+                                                          unsigned tile, unsigned sl, unsigned c) {
+    return (epoch << 32) | ((unsigned long long)(round & 0x3fffu) << 17) | (tile << 10) |
+           (sl << 6) | c;
+}
+__device__ __forceinline__ unsigned task_tile(unsigned long long task) {
+    return (unsigned)(task >> 10) & 0x7fu;
+}
+__device__ __forceinline__ bool task_dropped(EngineCtl* ctl, unsigned long long task) {
+    const unsigned c = (unsigned)task & 63u;
+    return ((unsigned)(task >> 17) & 0x3fffu) == (ld_agent(&ctl->done[c][1]) & 0x3fffu);
+}
+// the committer of component c has finished round `round`: drop what is left of its tiles
+__device__ __forceinline__ void engine_round_finished(EngineCtl* ctl, int c, unsigned round) {
+    __hip_atomic_store(&ctl->done[c][1], round & 0x3fffu, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void acquire_agent() {

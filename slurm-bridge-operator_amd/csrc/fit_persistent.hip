@@ -96,12 +96,15 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 for (unsigned i = lane; i < ntiles; i += 64) {
                     const unsigned idx = base + i;
                     const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
-                    const unsigned long long g = ((unsigned long long)(idx / QCAP + 1) << 32) |
-                                                 (tile << 10) | (sl << 6) | c;
+                    const unsigned long long g =
+                    engine_task(idx / QCAP + 1, (unsigned)rounds + 1u, tile, sl, (unsigned)c);
                     __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
                 target += ntiles;
+#ifdef FIT_STAMPS
+                if (lane == 0) ctl->pub[c] = __builtin_amdgcn_s_memrealtime();
+#endif
                 if (multi && !fail) fail = !wait_tiles(ctl, c, target);
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // node rows written by this block: CU-wide view for all waves
@@ -132,6 +135,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 R = CommitResult{M->res[0], M->res[1], M->res[2], M->res[3]};
                 __syncthreads();
             }
+            if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
             if (R.stop == 3) {  // commit watchdog
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
                 break;
@@ -145,7 +149,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             sr += R.stop == 1;
             sd += R.stop == 2;
             cursor += R.done;
-            const int nw = R.stop ? 2 * R.done : 2 * w;
+#ifndef ENGINE_WGROW
+#define ENGINE_WGROW 10  // next window after a stop, in eighths of the jobs the round resolved
+#endif
+            const int nw = R.stop ? (ENGINE_WGROW * R.done) / 8 : 2 * w;
             win = max(S.wmin, min(S.wmax, nw));
         }
         if (wave != 0) return;
@@ -161,7 +168,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
     unsigned long long* task_slot =
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
-    int64_t busy = 0;  // realtime ticks (100 MHz) spent scanning
+    int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
+    int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
     for (;;) {
         if (threadIdx.x == 0) {
             const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
@@ -183,28 +191,45 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (task != TASK_EXIT && task_dropped(ctl, task)) task |= TASK_SKIP;
             *task_slot = task;
         }
         __syncthreads();
         const unsigned long long task = *task_slot;
         if (task == TASK_EXIT) {  // block-uniform
-            if (threadIdx.x == 0) wbusy[blockIdx.x - ncomp] = busy;
+            if (threadIdx.x == 0) {
+                wbusy[2 * (blockIdx.x - ncomp)] = busy;
+                wbusy[2 * (blockIdx.x - ncomp) + 1] = scanned;
+            }
             return;
         }
         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-        if (threadIdx.x == 0) acquire_agent();
-        else __builtin_amdgcn_s_dcache_inv();
-        __syncthreads();
+        const bool skip = (task & TASK_SKIP) != 0ull;  // block-uniform
         const int c = (int)(task & 63u);
         const int s = (int)((task >> 6) & 15u);
-        const int tile = (int)((task >> 10) & 0x3fffffu);
-        const CompPlan P = plans[c];
-        scan_tile<true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,
-                        xk);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        const int tile = (int)task_tile(task);
+        if (!skip) {
+            if (threadIdx.x == 0) acquire_agent();
+            else __builtin_amdgcn_s_dcache_inv();
+            __syncthreads();
+            const CompPlan P = plans[c];
+            scan_tile<true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,
+                            xk);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+#ifdef FIT_STAMPS
+            if (threadIdx.x == 0 && tile == 0) {  // the round's first tile: pickup delay, scan time
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                atomicAdd(&g_mw[c][10], (unsigned long long)t0 - ctl->pub[c]);
+                atomicAdd(&g_mw[c][11], 1ull);
+                atomicAdd(&g_mw[c][12], now - (unsigned long long)t0);
+            }
+#endif
+            const int a = P.sb + s * SCAN_WAVES * P.sub, b = min(P.se, a + SCAN_WAVES * P.sub);
+            scanned += (int64_t)max(min(SCAN_JOBS, P.w - tile * SCAN_JOBS), 0) * max(b - a, 0);
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
-            release_agent();
+            if (!skip) release_agent();
             __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment

@@ -873,8 +873,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             for (unsigned i = lane; i < ntiles; i += 64) {
                 const unsigned idx = base + i;
                 const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
-                const unsigned long long g = ((unsigned long long)(idx / QCAP + 1) << 32) |
-                                             (tile << 10) | (sl << 6) | c;
+                const unsigned long long g =
+                    engine_task(idx / QCAP + 1, (unsigned)rounds + 1u, tile, sl, (unsigned)c);
                 __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -884,6 +884,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             const CommitResult r = commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd,
                                                        wjob, perm, out, outs, H, R,
                                                        &ctl->tdone[c][0], (unsigned)S.nslice);
+            if (lane == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
             if (r.stop == 3) {
                 fail = true;
                 break;
@@ -913,7 +914,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
     unsigned long long* task_slot =
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
-    int64_t busy = 0;  // realtime ticks (100 MHz) spent scanning
+    int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
+    int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
     for (;;) {
         if (threadIdx.x == 0) {
             const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
@@ -935,28 +937,37 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (task != TASK_EXIT && task_dropped(ctl, task)) task |= TASK_SKIP;
             *task_slot = task;
         }
         __syncthreads();
         const unsigned long long task = *task_slot;
         if (task == TASK_EXIT) {  // block-uniform
-            if (threadIdx.x == 0) wbusy[blockIdx.x - ncomp] = busy;
+            if (threadIdx.x == 0) {
+                wbusy[2 * (blockIdx.x - ncomp)] = busy;
+                wbusy[2 * (blockIdx.x - ncomp) + 1] = scanned;
+            }
             return;
         }
         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-        if (threadIdx.x == 0) acquire_agent();
-        else __builtin_amdgcn_s_dcache_inv();
-        __syncthreads();
+        const bool skip = (task & TASK_SKIP) != 0ull;  // block-uniform
         const int c = (int)(task & 63u);
         const int s = (int)((task >> 6) & 15u);
-        const int tile = (int)((task >> 10) & 0x3fffffu);
-        const CompPlan P = plans[c];
-        scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
-                     slot_min, xk);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        const int tile = (int)task_tile(task);
+        if (!skip) {
+            if (threadIdx.x == 0) acquire_agent();
+            else __builtin_amdgcn_s_dcache_inv();
+            __syncthreads();
+            const CompPlan P = plans[c];
+            scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
+                         slot_min, xk);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+            const int a = P.sb + s * SCAN_WAVES * P.sub, b = min(P.se, a + SCAN_WAVES * P.sub);
+            scanned += (int64_t)max(min(SCAN_JOBS, P.w - tile * SCAN_JOBS), 0) * max(b - a, 0);
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
-            release_agent();
+            if (!skip) release_agent();
             __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment

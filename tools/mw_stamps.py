@@ -22,6 +22,10 @@ tot = [sum(buf[c * 16 + i] for c in range(64)) for i in range(16)]
 dj, hj = max(tot[2], 1), max(tot[5], 1)
 print(f"decider: {tot[0] / dj:.0f} cyc/job, waiting for records {tot[1] / dj:.0f}, check+reduce {tot[7] / dj:.0f}, "
       f"decide+publish {tot[8] / dj:.0f} cyc/job")
+print(f"decider waits in the first {8} jobs of each round: {tot[9] / dj:.0f} cyc/job (of the total wait)")
+t0n = max(sum(buf[c * 16 + 11] for c in range(64)), 1)
+print(f"round's first tile: pickup delay {sum(buf[c * 16 + 10] for c in range(64)) / t0n / 100:.1f} us, "
+      f"scan {sum(buf[c * 16 + 12] for c in range(64)) / t0n / 100:.1f} us (per task, {t0n} tasks)")
 print(f"helpers: {tot[3] / hj:.0f} cyc/job (per helper), waiting for snapshot {tot[4] / hj:.0f}, "
       f"items/job {tot[6] / hj:.2f}")
 for c in range(64):
