@@ -700,9 +700,9 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
                                         "timeline engine's LDS", maxnodes);
     const int64_t wcap = std::min(c->wmax, 8192);
     int slices = TL_SLICES, tl_min_sub = TL_MIN_SUB;
-    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 4));
+    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 64 / TL_KS));
     if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
-    const int64_t per_comp_cand = wcap * slices * KS;
+    const int64_t per_comp_cand = wcap * slices * TL_KS;
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
         c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
         c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
@@ -811,7 +811,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     const size_t lds = commit_tl_lds_bytes(maxlen);
     const int runs = commit_tl_runs(maxlen);
     int slices = std::max(1, TL_SLICES / shards), tl_min_sub = TL_MIN_SUB;
-    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 512 / (KS * shards)));
+    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 512 / (TL_KS * shards)));
     if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
     if (runs < 1)
         return fail(FIT_E_INVAL, "partition component of %d nodes is too large for the timeline "
@@ -834,7 +834,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
             // the scan wants more waves in flight; candidate entries per job stay <= 256
             P.sub = std::max(tl_min_sub, (per + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
             P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
-            epl = std::max(epl, (shards * P.nslice * KS + 63) / 64);
+            epl = std::max(epl, (shards * P.nslice * TL_KS + 63) / 64);
             P.jbase = cur[k];
             P.w = std::min(win[k], jb[k + 1] - cur[k]);
             P.blk0 = (int32_t)blocks;
@@ -843,7 +843,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
             if (P.w > 0) {
                 any = true;
                 blocks += (int64_t)((P.w + SCAN_JOBS - 1) / SCAN_JOBS) * P.nslice;
-                cand_n += (int64_t)P.w * P.nslice * KS;
+                cand_n += (int64_t)P.w * P.nslice * TL_KS;
                 slots += P.w;
                 evals += (int64_t)P.w * (P.se - P.sb);
             }

@@ -52,38 +52,40 @@ __device__ __forceinline__ uint64_t wave_min_key(uint64_t v) {
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
 
-// sorted ascending insert of x into key[0..KS) dropping the largest (static indices only)
-__device__ __forceinline__ void topk_insert(uint64_t (&key)[KS], uint64_t x) {
+// sorted ascending insert of x into key[0..K) dropping the largest (static indices only)
+template <int K>
+__device__ __forceinline__ void topk_insert(uint64_t (&key)[K], uint64_t x) {
 #pragma unroll
-    for (int i = KS - 1; i > 0; --i) key[i] = umax64(key[i - 1], umin64(key[i], x));
+    for (int i = K - 1; i > 0; --i) key[i] = umax64(key[i - 1], umin64(key[i], x));
     key[0] = umin64(key[0], x);
 }
 
 // (list, bound) pairs: every node of the covered range that is not in the sorted list has a
 // key > bound, and every list entry is <= bound (bound = last entry, INF when not full).
 // Merge two such pairs over disjoint ranges into the pair for the union (bitonic, registers).
-__device__ __forceinline__ void merge_lists(uint64_t (&a)[KS], const uint64_t (&b)[KS]) {
-    const uint64_t bb = umin64(a[KS - 1], b[KS - 1]);
-    uint64_t c[KS];
+template <int K>
+__device__ __forceinline__ void merge_lists(uint64_t (&a)[K], const uint64_t (&b)[K]) {
+    const uint64_t bb = umin64(a[K - 1], b[K - 1]);
+    uint64_t c[K];
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
+    for (int i = 0; i < K; ++i) {
         const uint64_t x = a[i] > bb ? KEY_INF : a[i];
-        const uint64_t y = b[KS - 1 - i] > bb ? KEY_INF : b[KS - 1 - i];
-        c[i] = umin64(x, y);  // bitonic sequence holding the KS smallest of the union
+        const uint64_t y = b[K - 1 - i] > bb ? KEY_INF : b[K - 1 - i];
+        c[i] = umin64(x, y);  // bitonic sequence holding the K smallest of the union
     }
 #pragma unroll
-    for (int st = KS / 2; st >= 1; st >>= 1)
+    for (int st = K / 2; st >= 1; st >>= 1)
 #pragma unroll
-        for (int i = 0; i < KS; ++i)
+        for (int i = 0; i < K; ++i)
             if ((i & st) == 0) {
                 const uint64_t lo = umin64(c[i], c[i + st]), hi = umax64(c[i], c[i + st]);
                 c[i] = lo;
                 c[i + st] = hi;
             }
 #pragma unroll
-    for (int i = 0; i < KS; ++i) a[i] = c[i];
+    for (int i = 0; i < K; ++i) a[i] = c[i];
     // The bound stays "last entry": if bb is finite, the list achieving it is full with all its
-    // KS entries <= bb, so the merged list is full and c[KS-1] <= bb is the new bound.
+    // K entries <= bb, so the merged list is full and c[K-1] <= bb is the new bound.
 }
 
 __device__ __forceinline__ int find_comp(const CompPlan* __restrict__ plan, int ncomp, int b) {

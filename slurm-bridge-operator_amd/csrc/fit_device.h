@@ -4,11 +4,18 @@
 
 namespace fitgpu {
 
-constexpr int KS = 16;          // candidates kept per (job, block-slice) by fit_scan
+#ifndef FIT_KS
+#define FIT_KS 16
+#endif
+constexpr int KS = FIT_KS;      // candidates kept per (job, block-slice) by fit_scan
 constexpr int SCAN_WAVES = 8;   // waves per scan block; each walks one sub-slice of nodes
 constexpr int SCAN_JOBS = 64;   // jobs per scan block (lanes = jobs, shared by the 8 waves)
 constexpr int MIN_SUB = 256;    // minimum nodes per wave sub-slice
-constexpr int MAX_SLICES = 4;   // block-slices per job per rank (sub-slice grows past this)
+constexpr int MAX_SLICES = 64 / KS;  // block-slices per job per rank (sub-slice grows past this)
+#ifndef FIT_TL_KS
+#define FIT_TL_KS 4
+#endif
+constexpr int TL_KS = FIT_TL_KS;  // candidates per (job, block-slice) of the backfill scan
 constexpr int UCAP = 256;       // dirty-node capacity per component per round (4 per lane)
 constexpr int MAX_COMPONENT_NODES = 1 << 20;  // LDS dirty bitmap limit (128 KiB)
 constexpr uint64_t KEY_INF = ~0ull;
@@ -65,7 +72,7 @@ constexpr int TL_MAX_SLOTS = 1024;  // horizon limit (slots); the C5 horizon
 #define TL_UCAP_DEF 64
 #endif
 constexpr int TL_UCAP = TL_UCAP_DEF;  // dirty nodes per component per round (TL_UCAP / 64 per lane)
-constexpr int TL_SLICES = 4;        // block-slices per job (over all ranks) in the timeline scan
+constexpr int TL_SLICES = 64 / TL_KS;  // block-slices per job (over all ranks) in the timeline scan
 constexpr int TL_MIN_SUB = 32;      // minimum nodes per wave sub-slice in the timeline scan
 constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position
 constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;

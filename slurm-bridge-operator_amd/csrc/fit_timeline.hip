@@ -5,7 +5,7 @@
 // (Seg: end slot, cpu, mem, gpu) in a fixed per-node slab of TL_MAX_SLOTS entries in HBM (only
 // the used prefix is ever touched), plus a contiguous 96-B header per node (run count, column
 // ceilings, partition mask, first TL_HEAD runs) that the scan streams.  The speculative rounds are
-// the plain fit's (fit_common.h): k_scan_tl keeps the exact top-KS keys per (job, block-slice)
+// the plain fit's (fit_common.h): k_scan_tl keeps the exact top-TL_KS keys per (job, block-slice)
 // plus a bound against the round-start timelines; k_commit_tl walks the window in priority order
 // with a dirty set of at most TL_UCAP nodes (two per lane) whose run lists (and prefix minima)
 // live in LDS, re-evaluates them exactly per job and reserves each decision in place.
@@ -192,12 +192,12 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
 // Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices; each wave walks its
 // nodes in order.  Node headers (96 B, contiguous) stream in through two register sets with
 // vector loads two nodes ahead (in-order vmcnt, so the wait for node x never waits for x+1);
-// the rare walk past the header's runs reads the slab with scalar loads.  Top-KS lists, bound
+// the rare walk past the header's runs reads the slab with scalar loads.  Top-TL_KS lists, bound
 // and the LDS merge tree are k_scan's (fit_common.h).
 __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec& J, int32_t H,
-                                             const Seg* __restrict__ slab, uint64_t (&key)[KS],
+                                             const Seg* __restrict__ slab, uint64_t (&key)[TL_KS],
                                              unsigned long long& batches) {
-    const uint64_t cut = key[KS - 1];
+    const uint64_t cut = key[TL_KS - 1];
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
     TlWalk w{-1, 0, 0, 0, 0, KEY_INF,
              (h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu && J.mem <= h.mem &&
@@ -223,7 +223,7 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
                             J.wall, H, lim, (uint32_t)x);
         }
     }
-    if (w.key < key[KS - 1]) topk_insert(key, w.key);
+    if (w.key < key[TL_KS - 1]) topk_insert(key, w.key);
 }
 
 // One scan tile: SCAN_JOBS window jobs × block-slice s of the component (host-driven k_scan_tl
@@ -234,7 +234,7 @@ __device__ __forceinline__ void scan_tile_tl(
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
-    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[KS][64]) {
+    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[TL_KS][64]) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -253,9 +253,9 @@ __device__ __forceinline__ void scan_tile_tl(
     J.k = 1;
     J.pad = 0;
 
-    uint64_t key[KS];
+    uint64_t key[TL_KS];
 #pragma unroll
-    for (int i = 0; i < KS; ++i) key[i] = KEY_INF;
+    for (int i = 0; i < TL_KS; ++i) key[i] = KEY_INF;
     const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
     const int n1 = min(P.se, n0 + P.sub);
     unsigned long long batches = 0, longn = 0;
@@ -292,29 +292,29 @@ __device__ __forceinline__ void scan_tile_tl(
     for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
         if (wave >= h && wave < 2 * h) {
 #pragma unroll
-            for (int i = 0; i < KS; ++i) xk[wave - h][i][lane] = key[i];
+            for (int i = 0; i < TL_KS; ++i) xk[wave - h][i][lane] = key[i];
         }
         __syncthreads();
         if (wave < h) {
-            uint64_t o[KS];
+            uint64_t o[TL_KS];
 #pragma unroll
-            for (int i = 0; i < KS; ++i) o[i] = xk[wave][i][lane];
+            for (int i = 0; i < TL_KS; ++i) o[i] = xk[wave][i][lane];
             merge_lists(key, o);
         }
         __syncthreads();
     }
     if (wave != 0 || !active) return;
-    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KS;
+    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * TL_KS;
 #pragma unroll
-    for (int i = 0; i < KS; i += 2) {
+    for (int i = 0; i < TL_KS; i += 2) {
         ulonglong2 v;
         v.x = key[i];
         v.y = key[i + 1];
         *reinterpret_cast<ulonglong2*>(dst + i) = v;
     }
-    if (key[KS - 1] != KEY_INF)
+    if (key[TL_KS - 1] != KEY_INF)
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
-                  (unsigned long long)key[KS - 1]);
+                  (unsigned long long)key[TL_KS - 1]);
     if (s == 0) wjob[P.slot0 + t] = J;
 }
 
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
     const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
     const CompPlan* __restrict__ plan, int ncomp, uint64_t* __restrict__ cand,
     uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob, int32_t H, int32_t slot_min) {
-    __shared__ uint64_t xk[SCAN_WAVES / 2][KS][64];
+    __shared__ uint64_t xk[SCAN_WAVES / 2][TL_KS][64];
     const int c = find_comp(plan, ncomp, blockIdx.x);
     const CompPlan P = plan[c];
     const int local = blockIdx.x - P.blk0;
@@ -482,7 +482,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
 
-    const int per_rank = P.nslice * KS;
+    const int per_rank = P.nslice * TL_KS;
     const int E = nranks * per_rank;
     int64_t off[EPL];
     bool has[EPL];
@@ -911,9 +911,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     }
 
     // ======================================================================== scan worker
-    uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
+    uint64_t(*xk)[TL_KS][64] = reinterpret_cast<uint64_t(*)[TL_KS][64]>(smem);
     unsigned long long* task_slot =
-        reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
+        reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64);
     int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
     int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
     for (;;) {
@@ -1085,7 +1085,7 @@ size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
     const size_t commit = sizeof(Seg) * TL_MAX_SLOTS +
                           (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * engine_tl_runs(max_component_nodes) +
                           (size_t)((max_component_nodes + 31) / 32) * 4;
-    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16;
+    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16;
     return std::max(commit, scan);
 }
 
