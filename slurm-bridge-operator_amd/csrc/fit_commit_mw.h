@@ -34,7 +34,8 @@ constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
 #define MW_HSLEEP 2
 #endif
-static_assert(MAX_SLICES * KS <= 64, "one candidate entry per lane");
+constexpr int MW_EPL = (MAX_SLICES * KS + 63) / 64;  // candidate entries per helper lane
+static_assert(MW_EPL <= 2, "at most two candidate entries per lane");
 static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
 struct alignas(16) MwRow {  // dirty row, current state
@@ -234,21 +235,22 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
 #define MW_HSTEP(A, B_, C)                                                                     \
     {                                                                                          \
         if (t >= P.w) goto hdone;                                                              \
-        { /* node rows of job t+H's candidates (keys arrived last step) */                     \
-            const uint64_t k_ = kk[B_];                                                        \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) { /* job t+H's candidates' rows */ \
+            const uint64_t k_ = kk[B_][e];                                                     \
             const uint32_t p_ = k_ != KEY_INF ? (uint32_t)k_ : (uint32_t)P.nb;                 \
             const NodeRec r_ = ld_node(rec + p_);                                              \
-            rc[B_] = r_.cpu;                                                                   \
-            rm[B_] = r_.mem;                                                                   \
-            rg[B_] = r_.gpu;                                                                   \
-            ra[B_] = r_.avail;                                                                 \
-            rk[B_] = r_.mask;                                                                  \
-            ro[B_] = r_.orig;                                                                  \
+            rc[B_][e] = r_.cpu;                                                                \
+            rm[B_][e] = r_.mem;                                                                \
+            rg[B_][e] = r_.gpu;                                                                \
+            ra[B_][e] = r_.avail;                                                              \
+            rk[B_][e] = r_.mask;                                                               \
+            ro[B_][e] = r_.orig;                                                               \
         }                                                                                      \
         {                                                                                      \
             const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
             if (!mw_tile_ready(T, tt_, ready, S)) goto hdone;                                  \
-            kk[C] = has ? cand[eoff + (int64_t)tt_ * E] : KEY_INF;                             \
+            _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e)                                  \
+                kk[C][e] = has[e] ? cand[eoff[e] + (int64_t)tt_ * E] : KEY_INF;                \
             jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
             jbd[C] = bnd[P.slot0 + tt_];                                                       \
         }                                                                                      \
@@ -274,13 +276,13 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         const int nu_ = (int)lds_ld(&S->nu);                                                   \
         const JobRec& J_ = jr[A];                                                              \
         const uint64_t Bd_ = jbd[A];                                                           \
-        uint64_t x0;                                                                           \
-        {                                                                                      \
-            const uint64_t k_ = kk[A];                                                         \
+        uint64_t x0[MW_EPL];                                                                   \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) {                                   \
+            const uint64_t k_ = kk[A][e];                                                      \
             const bool ok_ = k_ <= Bd_ && k_ != KEY_INF;                                       \
             const uint32_t rel_ = ok_ ? (uint32_t)k_ - (uint32_t)P.nb : 0u;                    \
             const bool dirty_ = (S->bitmap[rel_ >> 5] >> (rel_ & 31)) & 1u;                    \
-            x0 = ok_ && !dirty_ ? k_ : KEY_INF;                                                \
+            x0[e] = ok_ && !dirty_ ? k_ : KEY_INF;                                             \
         }                                                                                      \
         uint64_t xd[UPL];                                                                      \
         MwRow wr_[UPL];                                                                        \
@@ -300,17 +302,22 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */ \
         const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
         for (; n_ < nmax_; ++n_) {                                                             \
-            uint64_t h_ = x0;                                                                  \
+            uint64_t h_ = x0[0];                                                               \
+            _Pragma("unroll") for (int e = 1; e < MW_EPL; ++e) h_ = umin64(h_, x0[e]);         \
             _Pragma("unroll") for (int i = 0; i < UPL; ++i) h_ = umin64(h_, xd[i]);            \
             const uint64_t best_ = wave_min_key(h_);                                           \
             if (best_ == KEY_INF) break;                                                       \
             const int w_ = __builtin_ctzll(__ballot(h_ == best_));                             \
             if (lane == w_) {                                                                  \
                 MwItem* it_ = &R_->it[n_];                                                     \
-                if (x0 == best_) {                                                             \
-                    *it_ = MwItem{best_, -1, ro[A], rc[A], rm[A], rg[A], ra[A], rk[A], 0, 0, 0}; \
-                    x0 = KEY_INF;                                                              \
-                } else {                                                                       \
+                bool cl_ = false;                                                              \
+                _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) if (x0[e] == best_) {       \
+                    *it_ = MwItem{best_, -1, ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e], \
+                                  rk[A][e], 0, 0, 0};                                          \
+                    x0[e] = KEY_INF;                                                           \
+                    cl_ = true;                                                                \
+                }                                                                              \
+                if (!cl_) {                                                                    \
                     _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (xd[i] == best_) {      \
                         *it_ = MwItem{best_, i * 64 + lane, wr_[i].orig, wr_[i].cpu,           \
                                       wr_[i].mem, wr_[i].gpu, wr_[i].avail, wr_[i].mask,       \
@@ -352,34 +359,42 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
     const int E = P.nslice * KS;
-    const bool has = lane < E;
-    const int64_t eoff = P.cand_off + (has ? lane : 0);
+    bool has[MW_EPL];       // candidate entry lane + 64 e of the job's E entries
+    int64_t eoff[MW_EPL];
+#pragma unroll
+    for (int e = 0; e < MW_EPL; ++e) {
+        has[e] = lane + 64 * e < E;
+        eoff[e] = P.cand_off + (has[e] ? lane + 64 * e : 0);
+    }
     const int wlast = P.w - 1;
     const int z = opaque_zero();
     int t = h - 1;
 
-    uint64_t kk[3], jbd[3];
+    uint64_t kk[3][MW_EPL], jbd[3];
     JobRec jr[3];
-    int32_t rc[3], rm[3], rg[3], ra[3], ro[3];
-    uint32_t rk[3];
+    int32_t rc[3][MW_EPL], rm[3][MW_EPL], rg[3][MW_EPL], ra[3][MW_EPL], ro[3][MW_EPL];
+    uint32_t rk[3][MW_EPL];
     int ready = 0;  // scan tiles known complete
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // jobs t and t + H
         const int tt = min(t + s * MW_H, wlast) + z;
         if (!mw_tile_ready(T, tt, ready, S)) return;  // halted / watchdog
-        kk[s] = has ? cand[eoff + (int64_t)tt * E] : KEY_INF;
+#pragma unroll
+        for (int e = 0; e < MW_EPL; ++e)
+            kk[s][e] = has[e] ? cand[eoff[e] + (int64_t)tt * E] : KEY_INF;
         jr[s] = ld_job(wjob + P.slot0 + tt);
         jbd[s] = bnd[P.slot0 + tt];
     }
-    {
-        const uint32_t p = kk[0] != KEY_INF ? (uint32_t)kk[0] : (uint32_t)P.nb;
+#pragma unroll
+    for (int e = 0; e < MW_EPL; ++e) {
+        const uint32_t p = kk[0][e] != KEY_INF ? (uint32_t)kk[0][e] : (uint32_t)P.nb;
         const NodeRec r = ld_node(rec + p);
-        rc[0] = r.cpu;
-        rm[0] = r.mem;
-        rg[0] = r.gpu;
-        ra[0] = r.avail;
-        rk[0] = r.mask;
-        ro[0] = r.orig;
+        rc[0][e] = r.cpu;
+        rm[0][e] = r.mem;
+        rg[0][e] = r.gpu;
+        ra[0][e] = r.avail;
+        rk[0][e] = r.mask;
+        ro[0][e] = r.orig;
     }
     MW_DECL(a_hw);
     MW_DECL(a_hn);

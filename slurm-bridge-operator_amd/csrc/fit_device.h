@@ -10,13 +10,22 @@ namespace fitgpu {
 constexpr int KS = FIT_KS;      // candidates kept per (job, block-slice) by fit_scan
 constexpr int SCAN_WAVES = 8;   // waves per scan block; each walks one sub-slice of nodes
 constexpr int SCAN_JOBS = 64;   // jobs per scan block (lanes = jobs, shared by the 8 waves)
-constexpr int MIN_SUB = 256;    // minimum nodes per wave sub-slice
-constexpr int MAX_SLICES = 64 / KS;  // block-slices per job per rank (sub-slice grows past this)
+#ifndef FIT_MIN_SUB
+#define FIT_MIN_SUB 64
+#endif
+constexpr int MIN_SUB = FIT_MIN_SUB;  // minimum nodes per wave sub-slice
+#ifndef FIT_MAX_SLICES
+#define FIT_MAX_SLICES (128 / FIT_KS)
+#endif
+constexpr int MAX_SLICES = FIT_MAX_SLICES;  // block-slices per job per rank (sub-slice grows past this)
 #ifndef FIT_TL_KS
 #define FIT_TL_KS 4
 #endif
 constexpr int TL_KS = FIT_TL_KS;  // candidates per (job, block-slice) of the backfill scan
-constexpr int UCAP = 256;       // dirty-node capacity per component per round (4 per lane)
+#ifndef FIT_UCAP
+#define FIT_UCAP 256
+#endif
+constexpr int UCAP = FIT_UCAP;       // dirty-node capacity per component per round (4 per lane)
 constexpr int MAX_COMPONENT_NODES = 1 << 20;  // LDS dirty bitmap limit (128 KiB)
 constexpr uint64_t KEY_INF = ~0ull;
 constexpr int FIT_KMAX = 8;     // nodes per multi-node job (include/fitgpu.h FIT_MAX_K)

@@ -272,6 +272,7 @@ hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, N
     else if (epl <= 2) FIT_COMMIT(2);
     else if (epl <= 4) FIT_COMMIT(4);
     else if (epl <= 8) FIT_COMMIT(8);
+    else if (epl <= 16) FIT_COMMIT(16);
     else return hipErrorInvalidValue;
 #undef FIT_COMMIT
     return hipGetLastError();

@@ -29,7 +29,7 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
                                                           const uint64_t* bnd, const JobRec* wjob,
                                                           int32_t* out, int kmax,
                                                           uint32_t* bitmap) {
-    return commit_window<1>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
+    return commit_window<MW_EPL>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
 }
 
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
