@@ -23,7 +23,10 @@
 
 namespace fitgpu {
 
-constexpr int MW_M = 8;                 // items per pre-resolved record (> snapshot lag)
+#ifndef MW_ITEMS
+#define MW_ITEMS 8
+#endif
+constexpr int MW_M = MW_ITEMS;          // items per pre-resolved record (> snapshot lag)
 constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once job t-8 is decided
 constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
 #ifndef MW_HELPERS
@@ -84,7 +87,8 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 #ifdef FIT_STAMPS
 // [comp][0] decider cycles, [1] decider wait-for-record, [2] decided jobs,
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
-// [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs
+// [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs,
+// [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record
 __device__ unsigned long long g_mw[64][16];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define MW_DECL(v) unsigned long long v = 0
@@ -248,7 +252,12 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         }                                                                                      \
         {                                                                                      \
             const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
+            MW_CLK(tw0_);                                                                      \
             if (!mw_tile_ready(T, tt_, ready, S)) goto hdone;                                  \
+            {                                                                                  \
+                MW_CLK(tw1_);                                                                  \
+                MW_ACC(a_ht, tw1_ - tw0_);                                                     \
+            }                                                                                  \
             _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e)                                  \
                 kk[C][e] = has[e] ? cand[eoff[e] + (int64_t)tt_ * E] : KEY_INF;                \
             jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
@@ -272,6 +281,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         {                                                                                      \
             MW_CLK(hw1_);                                                                      \
             MW_ACC(a_hw, hw1_ - hw0_);                                                         \
+            MW_ACC(a_hp, -(long long)hw1_);                                                    \
         }                                                                                      \
         const int nu_ = (int)lds_ld(&S->nu);                                                   \
         const JobRec& J_ = jr[A];                                                              \
@@ -339,6 +349,10 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
             *reinterpret_cast<uint4*>(&R_->h) =                                                \
                 make_uint4((uint32_t)t + 1u, v_, (uint32_t)n_, (uint32_t)J_.q);                 \
         }                                                                                      \
+        {                                                                                      \
+            MW_CLK(hp1_);                                                                      \
+            MW_ACC(a_hp, hp1_);                                                                \
+        }                                                                                      \
         MW_ACC(a_hn, 1);                                                                       \
         MW_ACC(a_hi, n_);                                                                      \
         t += MW_H;                                                                             \
@@ -399,6 +413,8 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     MW_DECL(a_hw);
     MW_DECL(a_hn);
     MW_DECL(a_hi);
+    MW_DECL(a_ht);  // waiting for scan tiles (prefetch of job t + 2H)
+    MW_DECL(a_hp);  // snapshot → record published
     MW_CLK(h0);
     for (;;) {
         MW_HSTEP(0, 1, 2)
@@ -411,6 +427,8 @@ hdone:;
     MW_ADD(4, a_hw);
     MW_ADD(5, a_hn);
     MW_ADD(6, a_hi);
+    MW_ADD(13, a_ht);
+    MW_ADD(14, a_hp);
 }
 #undef MW_HSTEP
 
