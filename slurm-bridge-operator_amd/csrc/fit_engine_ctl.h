@@ -28,27 +28,30 @@ __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Task word: {epoch:32 | skip:1 | round:14 | tile:7 | slice:4 | component:6}.  done[c][1] holds
+// Task word: {epoch:32 | skip:1 | round:12 | tile:7 | slice:6 | component:6}.  done[c][1] holds
 // the round tag of component c's last finished commit: a task of that round is dropped unscanned
 // (it only counts as done) — a round that stops early leaves its later tiles unneeded, and
 // scanning them would delay both the next round's start and other components' tiles.
 static_assert(ENGINE_TILES <= 128, "7 tile bits");
+__device__ __forceinline__ unsigned task_slice(unsigned long long task) {
+    return (unsigned)(task >> 6) & 0x3fu;  // up to 64 block-slices per job
+}
 constexpr unsigned long long TASK_SKIP = 1ull << 31;
 __device__ __forceinline__ unsigned long long engine_task(unsigned long long epoch, unsigned round,
                                                           unsigned tile, unsigned sl, unsigned c) {
-    return (epoch << 32) | ((unsigned long long)(round & 0x3fffu) << 17) | (tile << 10) |
+    return (epoch << 32) | ((unsigned long long)(round & 0xfffu) << 19) | (tile << 12) |
            (sl << 6) | c;
 }
 __device__ __forceinline__ unsigned task_tile(unsigned long long task) {
-    return (unsigned)(task >> 10) & 0x7fu;
+    return (unsigned)(task >> 12) & 0x7fu;
 }
 __device__ __forceinline__ bool task_dropped(EngineCtl* ctl, unsigned long long task) {
     const unsigned c = (unsigned)task & 63u;
-    return ((unsigned)(task >> 17) & 0x3fffu) == (ld_agent(&ctl->done[c][1]) & 0x3fffu);
+    return ((unsigned)(task >> 19) & 0xfffu) == (ld_agent(&ctl->done[c][1]) & 0xfffu);
 }
 // the committer of component c has finished round `round`: drop what is left of its tiles
 __device__ __forceinline__ void engine_round_finished(EngineCtl* ctl, int c, unsigned round) {
-    __hip_atomic_store(&ctl->done[c][1], round & 0x3fffu, __ATOMIC_RELAXED,
+    __hip_atomic_store(&ctl->done[c][1], round & 0xfffu, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -952,7 +952,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
         const bool skip = (task & TASK_SKIP) != 0ull;  // block-uniform
         const int c = (int)(task & 63u);
-        const int s = (int)((task >> 6) & 15u);
+        const int s = (int)task_slice(task);
         const int tile = (int)task_tile(task);
         if (!skip) {
             if (threadIdx.x == 0) acquire_agent();
