@@ -46,6 +46,7 @@ extern "C" {
 
 #define FIT_MAX_PARTITIONS 32
 #define FIT_MAX_K 8         /* nodes per job (--nodes) supported by fit_place              */
+#define FIT_MAX_NODES (1 << 29) /* node rows per fit_load_nodes (commit keys tag pos << 3)  */
 
 typedef struct fit_ctx fit_ctx;
 

@@ -1042,7 +1042,7 @@ void fit_destroy(fit_ctx* ctx) {
 int fit_load_nodes(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem,
                    const int32_t* gpu, const int32_t* av, const uint32_t* mask) {
     if (!c) return fail(FIT_E_INVAL, "null ctx");
-    if (n < 0 || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
+    if (n < 0 || n > FIT_MAX_NODES || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
         return fail(FIT_E_INVAL, "bad node arrays");
     HIP_TRY(hipSetDevice(c->device));
     if (alloc_cols(c, n)) return FIT_E_OOM;
@@ -1059,7 +1059,7 @@ int fit_load_nodes(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem
 int fit_load_nodes_device(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem,
                           const int32_t* gpu, const int32_t* av, const uint32_t* mask) {
     if (!c) return fail(FIT_E_INVAL, "null ctx");
-    if (n < 0 || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
+    if (n < 0 || n > FIT_MAX_NODES || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
         return fail(FIT_E_INVAL, "bad node arrays");
     HIP_TRY(hipSetDevice(c->device));
     if (alloc_cols(c, n)) return FIT_E_OOM;

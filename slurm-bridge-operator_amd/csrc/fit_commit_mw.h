@@ -88,7 +88,8 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 // [comp][0] decider cycles, [1] decider wait-for-record, [2] decided jobs,
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
 // [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs,
-// [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record
+// [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record,
+// [15] helper snapshot → extraction start
 __device__ unsigned long long g_mw[64][16];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define MW_DECL(v) unsigned long long v = 0
@@ -210,6 +211,38 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
     return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
 }
 
+// Helper entry lists: MW_EPL clean candidates + UPL dirty rows per lane, each key tagged with
+// its entry index in the low bits (positions < 2^29, FIT_MAX_NODES), INF stays INF.
+constexpr int MW_NE = MW_EPL + UPL;
+static_assert(MW_NE <= 8, "entry index takes 3 bits (and 4 bits of item index each in 32)");
+static_assert(MW_M <= 15, "item index + 1 fits 4 bits");
+__device__ __forceinline__ uint64_t mw_tag(uint64_t k, int e) {
+    return k == KEY_INF ? KEY_INF
+                        : (k & 0xffffffff00000000ull) | (uint32_t)(((uint32_t)k << 3) | (uint32_t)e);
+}
+__device__ __forceinline__ void mw_cas(uint64_t& a, uint64_t& b) {
+    const uint64_t lo = umin64(a, b), hi = umax64(a, b);
+    a = lo;
+    b = hi;
+}
+// ascending sort of a lane's entries (static indices only): the 12-comparator network for 6,
+// odd-even transposition otherwise
+template <int N>
+__device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
+    if constexpr (N == 6) {
+        mw_cas(q[0], q[5]); mw_cas(q[1], q[3]); mw_cas(q[2], q[4]);
+        mw_cas(q[1], q[2]); mw_cas(q[3], q[4]);
+        mw_cas(q[0], q[3]); mw_cas(q[2], q[5]);
+        mw_cas(q[0], q[1]); mw_cas(q[2], q[3]); mw_cas(q[4], q[5]);
+        mw_cas(q[1], q[2]); mw_cas(q[3], q[4]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+#pragma unroll
+            for (int i = r & 1; i + 1 < N; i += 2) mw_cas(q[i], q[i + 1]);
+    }
+}
+
 // Wait until job tt's scan tile is complete (uniform; `ready` = tiles known complete, they finish
 // roughly in order).  false: the decider halted / a watchdog tripped.
 __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& ready, MwShared* S) {
@@ -282,6 +315,7 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
             MW_CLK(hw1_);                                                                      \
             MW_ACC(a_hw, hw1_ - hw0_);                                                         \
             MW_ACC(a_hp, -(long long)hw1_);                                                    \
+            MW_ACC(a_hx, -(long long)hw1_);                                                    \
         }                                                                                      \
         const int nu_ = (int)lds_ld(&S->nu);                                                   \
         const JobRec& J_ = jr[A];                                                              \
@@ -309,34 +343,39 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         }                                                                                      \
         MwRec* R_ = &S->rec[t & (MW_R - 1)];                                                   \
         int n_ = 0;                                                                            \
-        /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */ \
-        const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
-        for (; n_ < nmax_; ++n_) {                                                             \
-            uint64_t h_ = x0[0];                                                               \
-            _Pragma("unroll") for (int e = 1; e < MW_EPL; ++e) h_ = umin64(h_, x0[e]);         \
-            _Pragma("unroll") for (int i = 0; i < UPL; ++i) h_ = umin64(h_, xd[i]);            \
-            const uint64_t best_ = wave_min_key(h_);                                           \
-            if (best_ == KEY_INF) break;                                                       \
-            const int w_ = __builtin_ctzll(__ballot(h_ == best_));                             \
-            if (lane == w_) {                                                                  \
-                MwItem* it_ = &R_->it[n_];                                                     \
-                bool cl_ = false;                                                              \
-                _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) if (x0[e] == best_) {       \
-                    *it_ = MwItem{best_, -1, ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e], \
-                                  rk[A][e], 0, 0, 0};                                          \
-                    x0[e] = KEY_INF;                                                           \
-                    cl_ = true;                                                                \
-                }                                                                              \
-                if (!cl_) {                                                                    \
-                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (xd[i] == best_) {      \
-                        *it_ = MwItem{best_, i * 64 + lane, wr_[i].orig, wr_[i].cpu,           \
-                                      wr_[i].mem, wr_[i].gpu, wr_[i].avail, wr_[i].mask,       \
-                                      0, 0, 0};                                                \
-                        xd[i] = KEY_INF;                                                       \
-                    }                                                                          \
-                }                                                                              \
-            }                                                                                  \
+        {                                                                                      \
+            MW_CLK(hx_);                                                                       \
+            MW_ACC(a_hx, hx_);                                                                 \
         }                                                                                      \
+        /* every entry tagged with its index (pos << 3 | e keeps the order of distinct nodes) and\
+           sorted per lane once; each extraction is then one wave minimum over the lane heads  \
+           plus a predicated shift in the winning lane, and the items are written in one pass */\
+        uint64_t q_[MW_NE];                                                                    \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) q_[e] = mw_tag(x0[e], e);           \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) q_[MW_EPL + i] = mw_tag(xd[i], MW_EPL + i);\
+        mw_sort(q_);                                                                           \
+        /* item index + 1 of each entry, 4 bits per entry (0: not taken) */                    \
+        uint32_t sel_ = 0u;                                                                    \
+        /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */  \
+        const int nmax_ = rfl(min(MW_M, t - (int)v_ + 1));                                     \
+        for (; n_ < nmax_; ++n_) {                                                             \
+            int wl_;                                                                           \
+            const uint64_t best_ = wave_min_key_lane(q_[0], wl_);                              \
+            if (best_ == KEY_INF) break;                                                       \
+            const bool me_ = lane == wl_;                                                      \
+            const uint32_t sv_ = (uint32_t)(n_ + 1) << (4u * ((uint32_t)best_ & 7u));          \
+            sel_ = me_ ? sel_ | sv_ : sel_;                                                    \
+            _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
+                q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
+            q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
+        }                                                                                      \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) if ((sel_ >> (4 * e)) & 15u)        \
+            R_->it[((sel_ >> (4 * e)) & 15u) - 1u] = MwItem{x0[e], -1, ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e],\
+                                     rk[A][e], 0, 0, 0};                                       \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) if ((sel_ >> (4 * (MW_EPL + i))) & 15u) \
+            R_->it[((sel_ >> (4 * (MW_EPL + i))) & 15u) - 1u] = MwItem{xd[i], i * 64 + lane, wr_[i].orig, wr_[i].cpu,   \
+                                              wr_[i].mem, wr_[i].gpu, wr_[i].avail, wr_[i].mask,\
+                                              0, 0, 0};                                        \
         if (lane == 0) {                                                                       \
             R_->h.cpu = J_.cpu;                                                                \
             R_->h.mem = J_.mem;                                                                \
@@ -415,6 +454,7 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     MW_DECL(a_hi);
     MW_DECL(a_ht);  // waiting for scan tiles (prefetch of job t + 2H)
     MW_DECL(a_hp);  // snapshot → record published
+    MW_DECL(a_hx);  // snapshot → extraction start (dirty rows read, candidates filtered)
     MW_CLK(h0);
     for (;;) {
         MW_HSTEP(0, 1, 2)
@@ -429,6 +469,7 @@ hdone:;
     MW_ADD(6, a_hi);
     MW_ADD(13, a_ht);
     MW_ADD(14, a_hp);
+    MW_ADD(15, a_hx);
 }
 #undef MW_HSTEP
 

@@ -49,6 +49,22 @@ __device__ __forceinline__ uint64_t wave_min_key(uint64_t v) {
     return ((uint64_t)mh << 32) | ml;
 }
 
+// wave_min_key plus the lane holding the minimum (the lowest such lane)
+__device__ __forceinline__ uint64_t wave_min_key_lane(uint64_t v, int& lane) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t mh = wave_min_u32(hi);
+    const uint64_t eq = __ballot(hi == mh);
+    uint32_t ml;
+    if (__popcll(eq) == 1) {
+        lane = __builtin_ctzll(eq);
+        ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, lane);
+    } else {
+        ml = wave_min_u32(hi == mh ? lo : 0xffffffffu);
+        lane = __builtin_ctzll(__ballot(hi == mh && lo == ml));
+    }
+    return ((uint64_t)mh << 32) | ml;
+}
+
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
 

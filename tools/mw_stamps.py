@@ -26,7 +26,8 @@ print(f"decider waits in the first {8} jobs of each round: {tot[9] / dj:.0f} cyc
 t0n = max(sum(buf[c * 16 + 11] for c in range(64)), 1)
 print(f"round's first tile: pickup delay {sum(buf[c * 16 + 10] for c in range(64)) / t0n / 100:.1f} us, "
       f"scan {sum(buf[c * 16 + 12] for c in range(64)) / t0n / 100:.1f} us (per task, {t0n} tasks)")
-print(f"helpers: tile waits {tot[13] / hj:.0f} cyc/job, snapshot -> record {tot[14] / hj:.0f} cyc/job")
+print(f"helpers: tile waits {tot[13] / hj:.0f} cyc/job, snapshot -> record {tot[14] / hj:.0f} cyc/job "
+      f"(of which snapshot -> extraction start {tot[15] / hj:.0f})")
 print(f"helpers: {tot[3] / hj:.0f} cyc/job (per helper), waiting for snapshot {tot[4] / hj:.0f}, "
       f"items/job {tot[6] / hj:.2f}")
 for c in range(64):
