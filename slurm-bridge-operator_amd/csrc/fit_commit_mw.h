@@ -28,11 +28,26 @@ namespace fitgpu {
 #endif
 constexpr int MW_M = MW_ITEMS;          // items per pre-resolved record (> snapshot lag)
 constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once job t-8 is decided
-constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
-#ifndef MW_HELPERS
-#define MW_HELPERS 7
+constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider [+ 1 recorder] + MW_H helpers
+// MW_RECORDER: wave 1 is the RECORDER — it takes the decider's decisions from a small LDS queue
+// and does their bookkeeping (dirty row, bitmap, placement, the {decided, nu} publish), which
+// leaves the decider's serial chain with the decision itself.  0: the decider does both.
+#ifndef MW_RECORDER
+#ifdef MW_DECIDER_BENCH
+#define MW_RECORDER 0
+#else
+#define MW_RECORDER 1
 #endif
-constexpr int MW_H = MW_HELPERS;  // 6: wave 4 (the decider's SIMD partner) stays idle
+#endif
+#ifndef MW_HELPERS
+#define MW_HELPERS (MW_RECORDER ? 6 : 7)
+#endif
+constexpr int MW_H = MW_HELPERS;  // waves 1 + MW_RECORDER .. MW_RECORDER + MW_H
+static_assert(MW_H + 1 + MW_RECORDER <= MW_WAVES, "one wave per role");
+constexpr int MW_DQ = 16;         // decision queue (decider -> recorder)
+#ifndef MW_PREFETCH
+#define MW_PREFETCH 0
+#endif
 constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
 #define MW_HSLEEP 2
@@ -76,6 +91,7 @@ struct alignas(16) MwShared {
     int32_t res[4];    // CommitResult of the window
     uint32_t pad[8];
     MwRec rec[MW_R];
+    uint4 dq[MW_DQ];  // decision of job t in dq[t % MW_DQ]: {t + 1, winner, slot, 0}
     MwRow rows[UCAP];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
 };
@@ -535,6 +551,22 @@ __device__ __forceinline__ void mw_read_rec(const MwRec* R, int i8, uint4& h0, u
     i2 = ip[2];
 }
 
+constexpr uint32_t MW_DQ_END = 0xfffffffeu;  // queue entry kind: the decider stopped here
+
+// Wait until the recorder has published job t - MW_DQ (queue entry t % MW_DQ is free).
+// false: the watchdog tripped (the failure flag is set).
+__device__ __forceinline__ bool mw_dq_space(MwShared* S, int t, int& dseen) {
+    for (unsigned sp = 0;; ++sp) {
+        dseen = rfl((int)lds_ld(&S->decided));
+        if (t < dseen + MW_DQ) return true;
+        if (sp > MW_SPIN_LIMIT || rfl((int)lds_ld(&S->fail))) {
+            lds_st(&S->fail, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(0);
+    }
+}
+
 // Out of line (as is mw_helper): called once per round, each gets its own register allocation
 // instead of sharing the persistent kernel's (which otherwise spills SGPRs in this loop).
 __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* Sin,
@@ -552,14 +584,34 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     int32_t wj = -1, ws = -1, wc = 0, wm = 0, wg = 0, wa = 0, wo = -1;  // written ring
     uint32_t wk = 0, wp = ~0u;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
+    int dseen = 0;             // jobs the recorder has published (last seen)
     MW_DECL(a_dw);
     MW_DECL(a_d0);  // waits of the round's first MW_R jobs (pipeline fill)
     MW_DECL(a_dc);
     MW_DECL(a_dd);
     MW_CLK(d0);
+#if MW_PREFETCH
+    // record t + 1 is read while job t is decided; one seen incomplete is read again in its turn
+    // (slot (t + 1) % MW_R is reused only for job t + 1 + MW_R, after job t + 2 is published)
+    uint4 p0, p1, p2, q0, q1, q2;
+    mw_read_rec(&S->rec[0], i8, p0, p1, p2, q0, q1, q2);
+#endif
     for (; t < P.w; ++t) {
         MW_CLK(dw0);
         uint4 h0, h1, h2, i0, i1, i2;
+#if MW_PREFETCH
+        h0 = p0, h1 = p1, h2 = p2, i0 = q0, i1 = q1, i2 = q2;
+        for (unsigned sp = 0; (uint32_t)rfl((int32_t)h0.x) != (uint32_t)t + 1u; ++sp) {
+            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {  // uniform exit
+                lds_st(&S->fail, 1u);
+                stop = 3;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(0);
+            mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
+        }
+        mw_read_rec(&S->rec[(t + 1) & (MW_R - 1)], i8, p0, p1, p2, q0, q1, q2);
+#else
         for (unsigned sp = 0;; ++sp) {  // speculative: header and items in one round trip
             mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
 #ifdef MW_DECIDER_BENCH
@@ -573,6 +625,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
             }
             __builtin_amdgcn_s_sleep(0);
         }
+#endif
         const MwHdr h{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
                       (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
                       ((uint64_t)h2.w << 32) | h2.z};
@@ -619,6 +672,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
             break;
         }
         int32_t node = -1;
+        int32_t dkind = -1, dslot = -1;  // winner for the recorder: item 0..7, 8 ring, -1 none
         if (best != KEY_INF) {
             int32_t sc, sm, sg, sa, slot;
             uint32_t sk;
@@ -649,7 +703,9 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
             const int32_t nm = sm - __builtin_amdgcn_readfirstlane(h.mem);
             const int32_t ng = sg - __builtin_amdgcn_readfirstlane(h.gpu);
             const uint32_t pos = (uint32_t)best;
-            if (lane == 0) {
+            dkind = rl >= 0 ? 8 : il >> 3;
+            dslot = slot;
+            if (!MW_RECORDER && lane == 0) {
                 S->rows[slot] = MwRow{nc, nm, ng, sa, sk, pos, node, t};
                 if (fresh) {
                     const uint32_t rel = pos - nb;
@@ -672,21 +728,40 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
             wo = writelane(node, e, wo);
             ++placed;
         }
-        oq = writelane(__builtin_amdgcn_readfirstlane(h.q), t & 63, oq);
-        ov = writelane(node, t & 63, ov);
-        if ((t & 63) == 63) {  // uniform: flush 64 placements
-            if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // global: vmcnt only
-            oq = -1;
+        if (MW_RECORDER) {
+            // queue entry t % MW_DQ is free once the recorder has published job t - MW_DQ
+            if (t >= dseen + MW_DQ && !mw_dq_space(S, t, dseen)) {
+                stop = 3;
+                break;
+            }
+            if (lane == 0)  // one 16-byte store: the recorder reads it with one load
+                *reinterpret_cast<uint4*>(&S->dq[t & (MW_DQ - 1)]) =
+                    make_uint4((uint32_t)t + 1u, (uint32_t)dkind, (uint32_t)dslot, 0u);
+        } else {
+            oq = writelane(__builtin_amdgcn_readfirstlane(h.q), t & 63, oq);
+            ov = writelane(node, t & 63, ov);
+            if ((t & 63) == 63) {  // uniform: flush 64 placements
+                if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // global: vmcnt only
+                oq = -1;
+            }
+            cbar();
+            if (lane == 0)  // {decided, nu} in one 8-byte LDS store
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
+                                   ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        cbar();
-        if (lane == 0)  // {decided, nu} in one 8-byte LDS store
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
-                               ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
         MW_CLK(dw3);
         MW_ACC(a_dd, dw3 - dw2);
     }
-    if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
+    if (MW_RECORDER) {  // end marker: the recorder finishes job t - 1 and reports `stop`
+        if (stop == 3 || t < dseen + MW_DQ || mw_dq_space(S, t, dseen)) {
+            if (lane == 0)
+                *reinterpret_cast<uint4*>(&S->dq[t & (MW_DQ - 1)]) =
+                    make_uint4((uint32_t)t + 1u, (uint32_t)MW_DQ_END, (uint32_t)stop, 0u);
+        }
+    } else if (oq >= 0 && lane < (t & 63)) {
+        ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
+    }
     if (stop) lds_st(&S->halt, 1u);
     MW_CLK(d1);
     MW_ADD(0, d1 - d0);
@@ -695,6 +770,96 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MW_ADD(9, a_d0);
     MW_ADD(7, a_dc);
     MW_ADD(8, a_dd);
+    return CommitResult{t, stop, nu, placed};
+}
+
+// ------------------------------------------------------------------------------ recorder
+// Takes the decisions in job order and does what the helpers and the output need: the dirty row
+// (current state, version t), the dirty bitmap bit of a fresh node, the placement (parked in lane
+// t & 63, stored 64 at a time), then {decided, nu} — the helpers' snapshot — in one 8-byte store
+// after the rest (DS order).  The winner's previous state comes from the record the decider used
+// (an item: its node did not change since the snapshot, or the decider would have dropped it) or
+// from the dirty row of a ring winner (this wave wrote it).  Record slot t % MW_R is reused only
+// for job t + MW_R, whose helper waits for decided >= t + 1: it is intact here.
+__device__ __noinline__ CommitResult mw_recorder(const CompPlan& Pref, MwShared* Sin,
+                                                 int32_t* __restrict__ out, int kmax) {
+    const CompPlan P = plan_sgpr(Pref);
+    MwShared* const S = lds_opaque(Sin);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nb = (uint32_t)P.nb;
+    int nu = 0, placed = 0, stop = 0, t = 0;
+    int32_t oq = -1, ov = -1;
+    for (;; ++t) {
+        uint4 d;
+        for (unsigned sp = 0;; ++sp) {
+            asm volatile("" ::: "memory");  // a fresh LDS read every spin
+            d = *reinterpret_cast<const uint4*>(&S->dq[t & (MW_DQ - 1)]);
+            if ((uint32_t)rfl((int32_t)d.x) == (uint32_t)t + 1u) break;
+            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {
+                lds_st(&S->fail, 1u);
+                stop = 3;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(0);
+        }
+        if (stop) break;
+        const uint32_t kind = (uint32_t)rfl((int32_t)d.y);
+        if (kind == MW_DQ_END) {
+            stop = rfl((int32_t)d.z);
+            break;
+        }
+        asm volatile("" ::: "memory");  // record / row reads after the queue entry's read
+        const MwRec* R = &S->rec[t & (MW_R - 1)];
+        const uint4 hq = reinterpret_cast<const uint4*>(&R->h)[0];  // {ready, v, n, q}
+        int32_t node = -1;
+        if (kind != 0xffffffffu) {
+            const uint4 hd = reinterpret_cast<const uint4*>(&R->h)[1];  // {cpu, mem, gpu, wall}
+            const int slot = rfl((int32_t)d.z);
+            uint4 a, b;
+            bool fresh = false;
+            if (kind < 8u) {  // record item: {key, tag, orig, cpu, mem, gpu, avail, mask, ...}
+                const uint4* ip = reinterpret_cast<const uint4*>(&R->it[kind]);
+                const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2];
+                fresh = rfl((int32_t)i0.z) < 0;
+                a = make_uint4(i1.x, i1.y, i1.z, i1.w);       // cpu, mem, gpu, avail
+                b = make_uint4(i2.x, i0.x, i0.w, (uint32_t)t);  // mask, pos, orig, version
+            } else {  // dirty row of a ring winner
+                const uint4* rp = reinterpret_cast<const uint4*>(&S->rows[slot]);
+                a = rp[0];
+                const uint4 r1 = rp[1];
+                b = make_uint4(r1.x, r1.y, r1.z, (uint32_t)t);
+            }
+            a.x = (uint32_t)((int32_t)a.x - (int32_t)hd.x);
+            a.y = (uint32_t)((int32_t)a.y - (int32_t)hd.y);
+            a.z = (uint32_t)((int32_t)a.z - (int32_t)hd.z);
+            node = rfl((int32_t)b.z);
+            if (lane == 0) {
+                uint4* rp = reinterpret_cast<uint4*>(&S->rows[slot]);
+                rp[0] = a;
+                rp[1] = b;
+                if (fresh) {
+                    const uint32_t rel = (uint32_t)rfl((int32_t)b.y) - nb;
+                    __hip_atomic_fetch_or(&S->bitmap[rel >> 5], 1u << (rel & 31),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            if (fresh) nu = slot + 1;
+            ++placed;
+        }
+        oq = writelane(rfl((int32_t)hq.w), t & 63, oq);
+        ov = writelane(node, t & 63, ov);
+        if ((t & 63) == 63) {  // uniform: flush 64 placements
+            if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;
+            oq = -1;
+        }
+        cbar();
+        if (lane == 0)  // {decided, nu} in one 8-byte LDS store, after the row and bitmap
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
+                               ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
+    if (stop) lds_st(&S->halt, 1u);
     return CommitResult{t, stop, nu, placed};
 }
 
@@ -710,6 +875,7 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
     if (threadIdx.x < MW_R) S->rec[threadIdx.x].h.ready = 0u;
+    if (threadIdx.x < MW_DQ) S->dq[threadIdx.x].x = 0u;
     if (threadIdx.x == 0) {
         S->decided = 0u;
         S->halt = 0u;
@@ -717,14 +883,17 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
         S->fail = 0u;
     }
     __syncthreads();
-    if (wave == 0) {
-        const CommitResult r = mw_decider(P, S, out, kmax);
-        if (threadIdx.x == 0) {
+    if (wave == 0 || (MW_RECORDER && wave == 1)) {
+        const CommitResult r = wave == 0 ? mw_decider(P, S, out, kmax)
+                                         : mw_recorder(P, S, out, kmax);
+        if (threadIdx.x == 64 * MW_RECORDER) {  // the recorder's result when it runs
             S->res[0] = r.done;
             S->res[1] = r.stop;
             S->res[2] = r.dirty;
             S->res[3] = r.placed;
         }
+    } else if (MW_RECORDER) {
+        mw_helper(P, S, rec, cand, bnd, wjob, wave - 1, T);  // waves 2.. : helpers 1..MW_H
     } else if (MW_H == MW_WAVES - 1) {
         mw_helper(P, S, rec, cand, bnd, wjob, wave, T);
     } else if (wave != 4) {
