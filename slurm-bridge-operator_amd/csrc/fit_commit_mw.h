@@ -45,9 +45,7 @@ constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider [+ 1 recorder] + MW_H helpe
 constexpr int MW_H = MW_HELPERS;  // waves 1 + MW_RECORDER .. MW_RECORDER + MW_H
 static_assert(MW_H + 1 + MW_RECORDER <= MW_WAVES, "one wave per role");
 constexpr int MW_DQ = 16;         // decision queue (decider -> recorder)
-#ifndef MW_PREFETCH
-#define MW_PREFETCH 0
-#endif
+
 constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
 #define MW_HSLEEP 2
@@ -105,8 +103,10 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
 // [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs,
 // [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record,
-// [15] helper snapshot → extraction start
-__device__ unsigned long long g_mw[64][16];
+// [15] helper snapshot → extraction start, [16] decider: records not ready at the first read,
+// [17] recorder cycles, [18] recorder waiting for decisions, [19] recorder jobs
+constexpr int MW_NSTAMP = 24;
+__device__ unsigned long long g_mw[64][MW_NSTAMP];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define MW_DECL(v) unsigned long long v = 0
 #define MW_ACC(v, x) v += (x)
@@ -585,33 +585,15 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     uint32_t wk = 0, wp = ~0u;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
     int dseen = 0;             // jobs the recorder has published (last seen)
+    MW_DECL(a_nr);
     MW_DECL(a_dw);
     MW_DECL(a_d0);  // waits of the round's first MW_R jobs (pipeline fill)
     MW_DECL(a_dc);
     MW_DECL(a_dd);
     MW_CLK(d0);
-#if MW_PREFETCH
-    // record t + 1 is read while job t is decided; one seen incomplete is read again in its turn
-    // (slot (t + 1) % MW_R is reused only for job t + 1 + MW_R, after job t + 2 is published)
-    uint4 p0, p1, p2, q0, q1, q2;
-    mw_read_rec(&S->rec[0], i8, p0, p1, p2, q0, q1, q2);
-#endif
     for (; t < P.w; ++t) {
         MW_CLK(dw0);
         uint4 h0, h1, h2, i0, i1, i2;
-#if MW_PREFETCH
-        h0 = p0, h1 = p1, h2 = p2, i0 = q0, i1 = q1, i2 = q2;
-        for (unsigned sp = 0; (uint32_t)rfl((int32_t)h0.x) != (uint32_t)t + 1u; ++sp) {
-            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {  // uniform exit
-                lds_st(&S->fail, 1u);
-                stop = 3;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(0);
-            mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
-        }
-        mw_read_rec(&S->rec[(t + 1) & (MW_R - 1)], i8, p0, p1, p2, q0, q1, q2);
-#else
         for (unsigned sp = 0;; ++sp) {  // speculative: header and items in one round trip
             mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
 #ifdef MW_DECIDER_BENCH
@@ -623,9 +605,9 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
                 stop = 3;
                 break;
             }
+            MW_ACC(a_nr, sp == 0);
             __builtin_amdgcn_s_sleep(0);
         }
-#endif
         const MwHdr h{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
                       (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
                       ((uint64_t)h2.w << 32) | h2.z};
@@ -770,6 +752,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MW_ADD(9, a_d0);
     MW_ADD(7, a_dc);
     MW_ADD(8, a_dd);
+    MW_ADD(16, a_nr);
     return CommitResult{t, stop, nu, placed};
 }
 
@@ -789,8 +772,11 @@ __device__ __noinline__ CommitResult mw_recorder(const CompPlan& Pref, MwShared*
     const uint32_t nb = (uint32_t)P.nb;
     int nu = 0, placed = 0, stop = 0, t = 0;
     int32_t oq = -1, ov = -1;
+    MW_DECL(a_rw);
+    MW_CLK(r0);
     for (;; ++t) {
         uint4 d;
+        MW_CLK(rw0);
         for (unsigned sp = 0;; ++sp) {
             asm volatile("" ::: "memory");  // a fresh LDS read every spin
             d = *reinterpret_cast<const uint4*>(&S->dq[t & (MW_DQ - 1)]);
@@ -803,6 +789,10 @@ __device__ __noinline__ CommitResult mw_recorder(const CompPlan& Pref, MwShared*
             __builtin_amdgcn_s_sleep(0);
         }
         if (stop) break;
+        {
+            MW_CLK(rw1);
+            MW_ACC(a_rw, rw1 - rw0);
+        }
         const uint32_t kind = (uint32_t)rfl((int32_t)d.y);
         if (kind == MW_DQ_END) {
             stop = rfl((int32_t)d.z);
@@ -860,6 +850,10 @@ __device__ __noinline__ CommitResult mw_recorder(const CompPlan& Pref, MwShared*
     }
     if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
     if (stop) lds_st(&S->halt, 1u);
+    MW_CLK(r1);
+    MW_ADD(17, r1 - r0);
+    MW_ADD(18, a_rw);
+    MW_ADD(19, t);
     return CommitResult{t, stop, nu, placed};
 }
 
