@@ -434,7 +434,9 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
-    const size_t lds = engine_lds_bytes(maxnodes);
+    size_t lds = engine_lds_bytes(maxnodes);
+    // experiment knob: a larger LDS request caps the blocks per CU (e.g. > 80 KB: one per CU)
+    if (const char* e = getenv("FIT_ENGINE_LDS_MIN")) lds = std::max(lds, (size_t)atol(e));
     int per_cu = engine_blocks_per_cu(lds);
     if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine does not fit on a CU (lds %zu)", lds);
     // Only the committers (blocks [0, nc), dispatched first) must be co-resident: a worker block
