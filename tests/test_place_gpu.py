@@ -99,3 +99,39 @@ def test_nodes_k_above_kmax_is_rejected():
         e.load_partitions(parts)
         with pytest.raises(FitError):
             e.place(jobs, kmax=2)
+
+
+# ---- commit hand-off patterns (decider / recorder / helpers) ----------------------
+def _uniform(n, j, cpu_node, cpu_job, mem_job=100, seed=0):
+    """n identical nodes, j jobs of cpu_job cpus (one partition): best fit packs one node at a time."""
+    rng = np.random.default_rng(seed)
+    nodes = synth.Nodes(np.full(n, cpu_node, np.int32), np.full(n, 1 << 20, np.int32),
+                        np.zeros(n, np.int32), np.full(n, synth.INT32_MAX, np.int32),
+                        np.ones(n, np.uint32))
+    cpu = np.asarray(cpu_job, np.int32) if np.ndim(cpu_job) else np.full(j, cpu_job, np.int32)
+    if cpu.size != j:
+        cpu = rng.choice(cpu, j).astype(np.int32)
+    jobs = synth.Jobs(cpu, np.full(j, mem_job, np.int32), np.zeros(j, np.int32),
+                      np.full(j, 60, np.int32), np.zeros(j, np.uint16), np.ones(j, np.uint16))
+    parts = synth.Partitions(np.full(1, -1, np.int32), np.full(1, -1, np.int32),
+                             np.full(1, -1, np.int32))
+    return nodes, jobs, parts
+
+
+@pytest.mark.parametrize("n,j,cpu_node,cpu_job", [
+    (64, 16384, 64, 1),          # every job lands on the node the previous one dirtied (ring winners)
+    (4096, 8192, 32, 32),        # every job fills a fresh node: dirty set full every 256 jobs
+    (1024, 20000, 96, [1, 2, 3, 5, 8, 13]),  # mixed sizes: items, ring entries and fresh nodes
+    (512, 20000, 64, [7, 64, 1]),  # cluster fills up: long tail of unplaced jobs
+])
+def test_commit_hand_off_patterns(n, j, cpu_node, cpu_job):
+    nodes, jobs, parts = _uniform(n, j, cpu_node, cpu_job)
+    check_parity(nodes, jobs, parts)
+
+
+def test_node_count_limit():
+    # commit keys tag positions as pos << 3 (FIT_MAX_NODES = 2^29 rows): larger tables are refused
+    from fitgpu import _lib
+    with Engine() as e:
+        assert _lib.lib().fit_load_nodes(e._h, (1 << 29) + 1, None, None, None, None, None) == \
+            _lib.FIT_E_INVAL
