@@ -20,6 +20,9 @@ namespace fitgpu {
 
 constexpr int TL_PM_STEPS = 32;     // LDS run lists hold <= 2 * TL_PM_STEPS = 64 runs
 constexpr int TL_UPL = TL_UCAP / 64;  // dirty slots per lane
+#ifndef TL_WAVE_WALKS
+#define TL_WAVE_WALKS 12 // walking LDS lists up to which a job walks them one at a time wave-wide
+#endif
 constexpr int32_t TL_BIG = 0x7fffffff;
 
 #ifdef FIT_STAMPS
@@ -361,6 +364,34 @@ __device__ __forceinline__ void tl_pm_build(const Seg* L, int4* PM, int n) {
     if (lane < n) PM[lane] = make_int4(vc, vm, vg, 0);
 }
 
+// The walk of tl_eval4 over an LDS run list of n <= 64 runs, by the whole wave (one run per
+// lane) instead of one lane: a window can only start where a maximal stretch of fitting runs
+// starts (slot 0 or the end of a run that does not fit), so the earliest window is the first run
+// w that fits and ends >= d slots after its stretch's start ra; its minima are those of the runs
+// from the stretch's first to w.  Same key as the serial walk (tl_step), including the `lim` cut.
+__device__ __forceinline__ uint64_t tl_walk_wave(const Seg* L, int n, int32_t jc, int32_t jm,
+                                                 int32_t jg, int32_t d, int32_t lim, uint32_t pos) {
+    const int lane = threadIdx.x & 63;
+    const bool v = lane < n;
+    const Seg g = v ? L[lane] : Seg{TL_BIG, 0, 0, 0};
+    const bool f = v && g.cpu >= jc && g.mem >= jm && g.gpu >= jg;
+    const uint64_t below = __ballot(!f) & ((1ull << lane) - 1ull);
+    const int sidx = below ? 64 - __builtin_clzll(below) : 0;  // first run of this lane's stretch
+    const int32_t pe = __shfl(g.end, max(sidx - 1, 0));
+    const int32_t ra = sidx ? pe : 0;
+    const uint64_t mw = __ballot(f && g.end - ra >= d);
+    if (!mw) return KEY_INF;
+    const int w = __builtin_ctzll(mw);
+    const int32_t st = __builtin_amdgcn_readlane(ra, w);
+    if (st > lim) return KEY_INF;
+    const int s0 = __builtin_amdgcn_readlane(sidx, w);
+    const bool in = lane >= s0 && lane <= w;
+    const int32_t mc = __builtin_amdgcn_readlane(wave_scan_min(in ? g.cpu : TL_BIG), 63);
+    const int32_t mm = __builtin_amdgcn_readlane(wave_scan_min(in ? g.mem : TL_BIG), 63);
+    const int32_t mg = __builtin_amdgcn_readlane(wave_scan_min(in ? g.gpu : TL_BIG), 63);
+    return tl_key(st, mc, mm, mg, jc, jm, jg, pos);
+}
+
 // Reserve (jc, jm, jg) on slots [s, e) of a run list, general form (any length, any address
 // space), by the whole wave: the runs from the one before the window to the end are split at s
 // and e into LDS scratch (prefix sums over piece counts), equal neighbours merge, and the result
@@ -588,7 +619,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
         // after d, by a 4-ary search (three rounds of three independent reads); a later start
         // (only when it can still win) or a global list walks the runs
         uint64_t dk[TL_UPL], dkm = KEY_INF;
-        bool walk[TL_UPL], anyw = false;
+        bool walk[TL_UPL], anyw = false, fit0 = false;
 #pragma unroll
         for (int i = 0; i < TL_UPL; ++i) {
             const bool dl = i * 64 + lane < nu && (umask[i] & jp) != 0u && jc <= ucc[i] &&
@@ -611,11 +642,22 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                     k += q * ((x1 < jd) + (x2 < jd) + (x3 < jd));
                 }
                 const int4 pk = pmr[(i * 64 + lane) * R + k];
-                if (pk.x >= jc && pk.y >= jm && pk.z >= jg)
+                if (pk.x >= jc && pk.y >= jm && pk.z >= jg) {
                     dk[i] = tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, upos[i]);
-                else
+                    fit0 = true;
+                } else {
                     walk[i] = cw == KEY_INF || (cw >> 54) > 0;
+                }
             }
+        }
+        // a walk of an LDS list only runs after its start-0 window failed, so it can only find a
+        // later start: once any dirty list fits from slot 0, those walks cannot win (global lists
+        // still walk, cut at start 0, as they may hold a better-scored start-0 window)
+        const bool any0 = __ballot(fit0) != 0;
+        uint64_t cutw = any0 ? 0ull : cw;
+#pragma unroll
+        for (int i = 0; i < TL_UPL; ++i) {
+            walk[i] = walk[i] && (uglob[i] || !any0);
             anyw = anyw || walk[i];
         }
         TL_CLK(c1b);
@@ -624,14 +666,28 @@ __device__ __forceinline__ CommitResult commit_tl_window(
 #ifdef FIT_STAMPS
             tacc[10] += 1;
 #endif
+            const int32_t wlim = cutw == KEY_INF ? H : (int32_t)(cutw >> 54);
 #pragma unroll
             for (int i = 0; i < TL_UPL; ++i) {
                 if (!__ballot(walk[i])) continue;
-                const uint64_t wl = tl_eval4(lr + (i * 64 + lane) * R, ucnt[i], R,
-                                             walk[i] && !uglob[i], jc, jm, jg, jd, H, upos[i], cw);
-                const uint64_t wg = tl_eval4(slab + (int64_t)upos[i] * TL_MAX_SLOTS, ucnt[i],
-                                             TL_MAX_SLOTS, walk[i] && uglob[i], jc, jm, jg, jd, H,
-                                             upos[i], cw);
+                // LDS lists: one wave-wide walk per walking list when few lists walk, else one
+                // lane per list (the serial walks run side by side)
+                uint64_t wl = KEY_INF;
+                const uint64_t mlds = __ballot(walk[i] && !uglob[i]);
+                if (__popcll(mlds) > TL_WAVE_WALKS) {
+                    wl = tl_eval4(lr + (i * 64 + lane) * R, ucnt[i], R, walk[i] && !uglob[i], jc,
+                                  jm, jg, jd, H, upos[i], cutw);
+                } else for (uint64_t mwl = mlds; mwl; mwl &= mwl - 1) {
+                    const int ll = __builtin_ctzll(mwl);
+                    const int n = __builtin_amdgcn_readlane(ucnt[i], ll);
+                    const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)upos[i], ll);
+                    const uint64_t k = tl_walk_wave(lr + (i * 64 + ll) * R, n, jc, jm, jg, jd, wlim, p);
+                    if (lane == ll) wl = k;
+                }
+                uint64_t wg = KEY_INF;
+                if (__ballot(walk[i] && uglob[i]))
+                    wg = tl_eval4(slab + (int64_t)upos[i] * TL_MAX_SLOTS, ucnt[i], TL_MAX_SLOTS,
+                                  walk[i] && uglob[i], jc, jm, jg, jd, H, upos[i], cutw);
                 dk[i] = walk[i] ? (uglob[i] ? wg : wl) : dk[i];
             }
         }
