@@ -1,23 +1,25 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json's headline metric on MI355X: placements/sec (+ job×node fit evals/sec)
-at 100k nodes × 1M jobs (config C3, 16 partitions) per GPU.
+at 100k nodes × 1M jobs (config C3, 16 partitions).
 
-N > 1 (default --scaling weak, SURVEY §8 e / DESIGN §3.5): the placement path partitions into
-independent partition components, so each rank places its own 100k × 1M cluster shard (a
-disjoint slice of the generator streams) with no collective in the data path; `value` is the
-aggregate placements/s of all ranks.  --scaling strong splits ONE 100k × 1M placement over the
-ranks instead (--shard-mode components | nodes: RCCL allgather + u64 min-allreduce per round).
+A "step" is one complete placement of the 1M-job stream against a freshly loaded 100k-node table,
+timed under BASELINE.md's rule — inputs already in HOST memory (pinned buffers, as a cgo caller
+would hand them over), wall time of fit_load_nodes + fit_place end to end (H2D, the placement,
+D2H of the placements).  That rate is `value`.  The same placement from HBM-resident inputs
+(fit_load_nodes_device + fit_place_device) is reported as `kernel_path_value`.
 
-A "step" is one complete placement of the 1M-job stream against a freshly loaded 100k-node table:
-fit_load_nodes_device (from HBM-resident columns) + fit_place_device.  Inputs are synthetic
-(splitmix64 generator, fitgpu/synth.py) and already resident in HBM when the timed region starts.
+N > 1 (default --scaling strong, --shard-mode nodes; SURVEY §8 e): ONE 100k × 1M placement split
+over the ranks by nodes, RCCL allgather of the candidate lists + u64 min-allreduce of the bounds
+per round.  --scaling weak gives every rank its own 100k × 1M cluster shard instead (no
+data-path collective; aggregate rate).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c3|c3o|c2|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  `roofline` is live: per-launch kernel time from the engine's HIP
-events (on the engine's stream), algorithmic work from DESIGN.md §5.  `cpu_baseline` times the
-oracle (C restatement of the scalar path, 1 thread) on a bounded prefix of the same workload.
+events (on the engine's stream), algorithmic work from DESIGN.md §5; `traffic` comes from the
+committed PMC profile named in `traffic_source`.  `cpu_baseline` times the CPU restatements
+(oracle/: naive port, component-aware, multicore) on bounded samples of the same workload.
 """
 from __future__ import annotations
 
@@ -36,6 +38,7 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU × 4 SI
 PEAK_HBM_GBS = 8000.0
 SCAN_OPS_PER_EVAL = 12    # algorithmic int32 ops per (job, node) fit eval
 SCAN_BYTES_PER_EVAL = 20  # algorithmic node-row bytes per eval (pre-reuse)
+CPU_THREADS = 16          # the GPU box's CPU share for one GPU (OMP_NUM_THREADS there)
 
 
 def commit_bytes_per_job(entries: int) -> int:
@@ -62,6 +65,7 @@ def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_comm
             "hbm_gbs_algorithmic": round(evals_local / steps * SCAN_BYTES_PER_EVAL / (ms * 1e-3) / 1e9, 1),
             "scan_worker_busy_ms": round(agg["ms_scan"] / steps, 3),
             "commit_chain_ms": round(agg["ms_commit"] / steps, 3),
+            "commit_ns_per_job": round(agg["ms_commit"] * 1e6 / max(jobs_resolved, 1), 1),
             "rounds_longest_component": agg["rounds"] / steps}}
     scan_ms = agg["ms_scan"] / rounds
     commit_ms = agg["ms_commit"] / rounds
@@ -75,8 +79,8 @@ def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_comm
                    "frac": round(scan_tops / PEAK_VALU_TOPS, 4),
                    "hbm_gbs_algorithmic": round(evals_per_launch * SCAN_BYTES_PER_EVAL / (scan_ms * 1e-3) / 1e9, 1)},
         names[1]: {"ms_per_launch": round(commit_ms, 4), "launches": rounds, "bound": "latency",
-                     "achieved": round(commit_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(commit_gbs / PEAK_HBM_GBS, 5)},
+                   "achieved": round(commit_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(commit_gbs / PEAK_HBM_GBS, 5)},
     }
 
 
@@ -85,22 +89,33 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
-                    help="c3: BASELINE headline (100k x 1M); c5: the same with a 1,024-slot backfill horizon")
-    ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="jobs in the CPU baseline sample (default 40,000; c5: 3,000)")
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5"],
+                    help="c3: BASELINE headline (100k x 1M); c3o: c3 + an all-nodes partition (one "
+                         "component); c5: c3 with a 1,024-slot backfill horizon")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-scale", type=float, default=1.0, help="scale the CPU-baseline samples (tests)")
+    ap.add_argument("--no-device-path", action="store_true", help="skip the HBM-resident rate")
     ap.add_argument("--rehearse", action="store_true",
                     help="test only: every rank on cuda:0 with gloo (rehearse N>1 on a 1-GPU box)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/gpu_pmc.sh + tools/pmc_json.py) with HBM bytes/launch")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = every rank places its own 100k x 1M cluster shard (independent "
-                         "partition components, no data-path collective); strong = one 100k x 1M "
-                         "placement split over the ranks (--shard-mode)")
-    ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
-                    help="strong scaling split: auto = partition components when there are >= N of them")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N>1: strong = one 100k x 1M placement split over the ranks (--shard-mode); "
+                         "weak = every rank places its own 100k x 1M cluster shard (no data-path collective)")
+    ap.add_argument("--shard-mode", default="nodes", choices=["auto", "nodes", "components"],
+                    help="strong scaling split (north_star: nodes)")
     return ap.parse_args()
+
+
+def _pinned(keep, a):
+    """Copy of numpy array `a` in page-locked host memory (what a caller would hand the C-ABI)."""
+    import torch
+    a = np.ascontiguousarray(a)
+    view = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32}.get(a.dtype)
+    t = torch.from_numpy(a.view(view) if view else a).pin_memory()
+    keep.append(t)
+    out = t.numpy()
+    return out.view(a.dtype) if view else out
 
 
 def main():
@@ -114,9 +129,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world != a.gpus and world == 1 and a.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     if a.rehearse:
         local = 0
         if a.scaling != "weak":
@@ -141,6 +155,35 @@ def main():
         nodes, tline, jobs, parts = synth.make_c5(shard=shard)
     else:
         nodes, jobs, parts = synth.make_config(a.workload, shard=shard)
+    kmax = 1
+
+    mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
+    if weak:
+        eng = Engine(device=local)  # independent shard: no collective in the data path
+    else:
+        eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
+    eng.load_partitions(parts)
+
+    # ---- host-memory path (BASELINE.md timing rule): pinned inputs, H2D ... D2H per step ------------
+    keep = []
+    h_nodes = synth.Nodes(*(_pinned(keep, x) for x in (nodes.cpu_free, nodes.mem_free, nodes.gpu_free,
+                                                        nodes.avail_min, nodes.part_mask)))
+    h_jobs = synth.Jobs(*(_pinned(keep, x) for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part,
+                                                      jobs.nodes_k)))
+    h_out = _pinned(keep, np.zeros(jobs.j * kmax, np.int32))
+    if tl:
+        h_tline = synth.Timeline(tline.slots, tline.slot_min,
+                                 *(_pinned(keep, x) for x in (tline.off, tline.slot, tline.cpu, tline.mem, tline.gpu)))
+        h_start = _pinned(keep, np.zeros(jobs.j, np.int32))
+
+    def step_host():
+        eng.load_nodes(h_nodes)
+        if tl:
+            eng.load_timeline(h_tline)
+            return eng.place_tl(h_jobs, node=h_out, start=h_start)[2]
+        return eng.place(h_jobs, kmax=kmax, out=h_out)[1]
+
+    # ---- HBM-resident path (kernel_path_value) --------------------------------------------------
     dev = torch.device("cuda", local)
     T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
     d_nodes = [T(nodes.cpu_free), T(nodes.mem_free), T(nodes.gpu_free), T(nodes.avail_min),
@@ -152,44 +195,42 @@ def main():
         d_rel = [T(x) for x in (tline.off, tline.slot, tline.cpu, tline.mem, tline.gpu)]
         d_start = torch.empty(jobs.j, dtype=torch.int32, device=dev)
 
-    mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
-    if weak:
-        eng = Engine(device=local)  # independent shard: no collective in the data path
-    else:
-        eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
-    eng.load_partitions(parts)
-
-    def step():
+    def step_dev():
         eng.load_nodes_device(*d_nodes)
         if tl:
             eng.load_timeline_device(tline.slots, tline.slot_min, *d_rel)
             return eng.place_tl_device(*d_jobs[:5], d_out, d_start)
-        return eng.place_device(*d_jobs, d_out, kmax=1)
+        return eng.place_device(*d_jobs, d_out, kmax=kmax)
 
-    for _ in range(a.warmup):
-        step()
-    stats = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        stats.append(step())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
     cdev = torch.device("cpu") if a.rehearse else dev  # gloo reduces CPU tensors
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
 
-    # output sanity every run: the engine's counts are internally consistent
-    s0 = stats[-1]
-    assert s0["placed"] + s0["unplaced"] + s0["rejected"] == jobs.j
+    def timed(step):
+        for _ in range(a.warmup):
+            step()
+        stats = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            stats.append(step())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, stats
 
-    value = jobs.j * a.steps / el * (world if weak else 1)
+    el, stats_host = timed(step_host)
+    s0 = stats_host[-1]
+    assert s0["placed"] + s0["unplaced"] + s0["rejected"] == jobs.j  # output sanity every run
+    mult = world if weak else 1
+    value = jobs.j * a.steps / el * mult
+    el_dev, stats = (None, stats_host) if a.no_device_path else timed(step_dev)
+
     agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan", "ms_commit",
                                                   "ms_exchange", "ms_device", "placed", "unplaced")}
     evals_local = agg["evals"]
@@ -197,6 +238,7 @@ def main():
         t = torch.tensor([float(agg["evals"]), float(agg["useful_evals"])], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
         agg["evals"], agg["useful_evals"] = int(t[0].item()), int(t[1].item())
+    el_k = el_dev if el_dev is not None else el
     used_mode = {0: "1 GPU", 1: f"node-sharded x{world} (RCCL allgather + u64 min-allreduce per round)",
                  2: f"partition-component-sharded x{world} (one RCCL merge)"}[stats[-1]["shard_mode"]]
     if weak:
@@ -206,54 +248,89 @@ def main():
                            "k_engine_tl" if tl else "k_engine")
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_launch"] * kernels[k]["launches"])
     k = kernels[dominant]
-    traffic = None
+    traffic, traffic_src = None, None
     if a.pmc_json and os.path.exists(a.pmc_json):
-        traffic = json.load(open(a.pmc_json)).get(dominant, {}).get("hbm_bytes_per_launch")
+        pmc = json.load(open(a.pmc_json))
+        traffic = pmc.get(dominant, {}).get("hbm_bytes_per_launch")
+        traffic_src = f"{os.path.relpath(a.pmc_json, ROOT)} ({pmc.get('source', '?')})" if traffic else None
     roofline = {"kernel": dominant, "bound": k["bound"], "achieved": k["achieved"], "peak": k["peak"],
-                "unit": k["unit"], "frac": k["frac"], "traffic": traffic}
+                "unit": k["unit"], "frac": k["frac"], "traffic": traffic, "traffic_source": traffic_src}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        from oracle import pyoracle as po
-        sample = min(a.cpu_sample or (3000 if tl else 40000), jobs.j)
-        sub = synth.Jobs(*(x[:sample] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part,
-                                                  jobs.nodes_k)))
-        t = time.perf_counter()
-        if tl:
-            _, _, cst, _ = po.ref_place_tl(nodes, tline, sub, parts)
-            what = "oracle/fitref_tl.c ref_place_tl (C restatement of SPEC §2b, dense timelines)"
-        else:
-            _, cst, _ = po.ref_place(nodes, sub, parts)
-            what = "oracle/fitref.c ref_place (C restatement of the scalar sequential path)"
-        ct = time.perf_counter() - t
-        cpu = {"value": round(sample / ct, 2), "unit": "placements/s", "cores": 1, "kind": "port",
-               "evals_per_s": round(cst["evals"] / ct, 1),
-               "sample": f"first {sample} jobs of {a.workload} vs all {nodes.n} nodes, {what}, 1 thread, "
-                         f"{ct:.1f}s",
-               "host_cpu": _cpu_model()}
+        cpu = cpu_baseline(a.workload, nodes, jobs, parts, tline if tl else None, a.cpu_scale)
 
+    resolved = s0["placed"] + s0["unplaced"]
     line = {
         "metric": base["metric"], "value": round(value, 1), "unit": "placements/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak" if (weak or world == 1) else "strong", "vs_baseline": None, "dtype": "int32",
-        "data": "synthetic (splitmix64 generator, fitgpu/synth.py; DESIGN.md §5)",
-        "config": {"workload": a.workload, "nodes": nodes.n * (world if weak else 1),
-                   "jobs": jobs.j * (world if weak else 1), "partitions": parts.p * (world if weak else 1),
-                   "per_gpu": {"nodes": nodes.n, "jobs": jobs.j} if weak else None,
+        "higher_is_better": True, "scaling": "weak" if (weak or world == 1) else "strong", "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (splitmix64 generator, fitgpu/synth.py; DESIGN.md §5); inputs in pinned host "
+                "memory, timed H2D..D2H (BASELINE.md timing rule)",
+        "config": {"workload": a.workload, "nodes": nodes.n * mult, "jobs": jobs.j * mult,
+                   "partitions": parts.p * mult, "per_gpu": {"nodes": nodes.n, "jobs": jobs.j} if weak else None,
                    **({"slots": tline.slots, "slot_min": tline.slot_min} if tl else {}),
                    "parallelism": used_mode, "components": stats[-1]["components"]},
-        "fit_evals_per_s": {"useful": round(agg["useful_evals"] / el, 1), "performed": round(agg["evals"] / el, 1)},
+        "kernel_path_value": round(jobs.j * a.steps / el_dev * mult, 1) if el_dev else None,
+        "kernel_path_ms_per_step": round(el_dev / a.steps * 1e3, 3) if el_dev else None,
+        "placed_plus_unplaced_per_s": round(resolved * a.steps / el * mult, 1),
+        "jobs": {"placed": s0["placed"], "unplaced": s0["unplaced"], "rejected_by_prefilter": s0["rejected"]},
+        "fit_evals_per_s": {"useful": round(agg["useful_evals"] / el_k, 1),
+                            "performed": round(agg["evals"] / el_k, 1)},
         "rounds_per_step": agg["rounds"] / a.steps,
         "round_stops_per_step": {"rescan": stats[-1]["stops_rescan"], "dirty_full": stats[-1]["stops_dirty"]},
         "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
     }
     if cpu:
-        line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        line["speedup_vs_cpu"] = {v["kind"]: round(value / v["value"], 1) for v in cpu["variants"]}
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
+    """The CPU paths on this host (rank 0, N = 1), each on a bounded sample of the same workload:
+    the naive port (oracle/fitref*.c, every node per job, 1 thread), the component-aware scan
+    (oracle/cpu_baseline.c, 1 thread) and the same on CPU_THREADS threads (components in parallel).
+    Per-job cost is flat in J, so each sample's rate stands for the whole stream."""
+    from fitgpu import synth
+    from oracle import pyoracle as po
+    threads = max(1, min(CPU_THREADS, os.cpu_count() or 1))
+
+    def prefix(m):
+        m = max(1, min(int(m * scale), jobs.j))
+        return m, synth.Jobs(*(x[:m] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part, jobs.nodes_k)))
+
+    if tline is not None:
+        runs = [("naive-port", 1, 2000, lambda s: po.ref_place_tl(nodes, tline, s, parts)[2],
+                 "oracle/fitref_tl.c ref_place_tl (SPEC §2b, dense timelines, every node per job)"),
+                ("component-aware", 1, 6000, lambda s: po.cpu_place_tl(nodes, tline, s, parts, 1)[2],
+                 "oracle/cpu_baseline.c cpu_place_tl (own component's nodes only)"),
+                ("multicore", threads, 60000, lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads)[2],
+                 f"oracle/cpu_baseline.c cpu_place_tl, components on {threads} threads")]
+    else:
+        runs = [("naive-port", 1, 20000, lambda s: po.ref_place(nodes, s, parts)[1],
+                 "oracle/fitref.c ref_place (C restatement of the scalar sequential path, every node per job)"),
+                ("component-aware", 1, 200000, lambda s: po.cpu_place(nodes, s, parts, 1)[1],
+                 "oracle/cpu_baseline.c cpu_place (own component's nodes only, vectorised scan)"),
+                ("multicore", threads, 1_000_000, lambda s: po.cpu_place(nodes, s, parts, threads)[1],
+                 f"oracle/cpu_baseline.c cpu_place, components on {threads} threads")]
+    variants = []
+    for kind, cores, m, fn, what in runs:
+        m, sub = prefix(m)
+        t = time.perf_counter()
+        st = fn(sub)
+        ct = time.perf_counter() - t
+        variants.append({"kind": kind, "value": round(m / ct, 1), "unit": "placements/s", "cores": cores,
+                         "evals_per_s": round(st["evals"] / ct, 1),
+                         "sample": f"first {m} jobs of {workload} vs all {nodes.n} nodes, {what}, {ct:.2f}s"})
+    best = max(variants, key=lambda v: v["value"])
+    return {"value": best["value"], "unit": "placements/s", "cores": best["cores"], "kind": "port",
+            "variant": best["kind"], "sample": best["sample"], "host_cpu": _cpu_model(),
+            "variants": variants}
 
 
 def _cpu_model() -> str:

@@ -67,10 +67,15 @@ typedef struct {
     int32_t shard_mode;   /* FIT_SHARD_*: how world > 1 ranks split one placement           */
     int32_t window_min;   /* jobs per component per round, lower bound (0 = default 256)   */
     int32_t window_max;   /* upper bound (0 = default 8192)                                 */
-    int32_t flags;        /* reserved, 0                                                    */
+    int32_t flags;        /* FIT_FLAG_* bits, 0 = none                                      */
     fit_exchange_fn exchange;  /* NULL = RCCL over xGMI (nccl_id required)                  */
     void* exchange_user;
 } fit_opts;
+
+/* fit_opts.flags: run the multi-rank code path (shard split, per-round exchange, merge) even at
+ * world == 1, over a one-rank RCCL communicator (or the host exchange): exercises the collective
+ * calls on a single GPU.  Placements are identical to the default path. */
+#define FIT_FLAG_COLLECTIVES 1
 
 #define FIT_SHARD_AUTO 0       /* components if there are at least `world` of them, else nodes */
 #define FIT_SHARD_NODES 1      /* every rank scans 1/world of every component's nodes; per     */

@@ -19,7 +19,8 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "liboracle.so")
-        srcs = [os.path.join(_HERE, f) for f in ("fitref.c", "fitref_tl.c", "round_model.c", "fitref.h", "Makefile")]
+        srcs = [os.path.join(_HERE, f) for f in ("fitref.c", "fitref_tl.c", "round_model.c", "cpu_baseline.c",
+                                                 "fitref.h", "Makefile")]
         if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
             subprocess.check_call(["make", "-s", "-C", _HERE])
         _LIB = C.CDLL(path)
@@ -127,3 +128,41 @@ def ref_place_tl(nodes, tline, jobs, parts, tl=None):
         raise ValueError("ref_place_tl: invalid input")
     stats = dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3]))
     return node, start, stats, tl
+
+
+# ---- fair CPU baselines (oracle/cpu_baseline.c; bench.py cpu_baseline leg) -----------------------
+def cpu_place(nodes, jobs, parts, threads: int = 1):
+    """Component-aware sequential best fit (k = 1), components on `threads` threads.  Same result
+    as ref_place.  Returns (out[J] int32, stats dict, final (cpu, mem, gpu))."""
+    cf, mf, gf, av, mk, pt, jb, jp, _ = _prep(nodes, jobs, parts)
+    out = np.empty(jobs.j, np.int32)
+    st = np.zeros(4, np.int64)
+    I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
+    rc = lib().cpu_place(
+        I32(nodes.n), _p(cf, I32), _p(mf, I32), _p(gf, I32), _p(av, I32), _p(mk, U32),
+        I32(parts.p), _p(pt[0], I32), _p(pt[1], I32), _p(pt[2], I32),
+        I32(jobs.j), _p(jb[0], I32), _p(jb[1], I32), _p(jb[2], I32), _p(jb[3], I32), _p(jp, U16),
+        _p(out, I32), _p(st, C.c_int64), I32(threads))
+    if rc != 0:
+        raise ValueError("cpu_place: invalid input")
+    return out, dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3])), (cf, mf, gf)
+
+
+def cpu_place_tl(nodes, tline, jobs, parts, threads: int = 1, tl=None):
+    """Component-aware SPEC §2b backfill on `threads` threads.  Same result as ref_place_tl."""
+    tl = ref_build_timeline(nodes, tline) if tl is None else np.ascontiguousarray(tl, np.int32).copy()
+    I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
+    mk = np.ascontiguousarray(nodes.part_mask, np.uint32)
+    pt = [np.ascontiguousarray(a, np.int32) for a in (parts.max_time_min, parts.max_cpus_per_node,
+                                                      parts.max_mem_per_node)]
+    jb = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
+    jp = np.ascontiguousarray(jobs.part, np.uint16)
+    node = np.empty(jobs.j, np.int32)
+    start = np.empty(jobs.j, np.int32)
+    st = np.zeros(4, np.int64)
+    rc = lib().cpu_place_tl(I32(nodes.n), I32(tline.slots), I32(tline.slot_min), _p(tl, I32), _p(mk, U32),
+                            I32(parts.p), *(_p(a, I32) for a in pt), I32(jobs.j), *(_p(a, I32) for a in jb),
+                            _p(jp, U16), _p(node, I32), _p(start, I32), _p(st, C.c_int64), I32(threads))
+    if rc != 0:
+        raise ValueError("cpu_place_tl: invalid input")
+    return node, start, dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3])), tl

@@ -188,6 +188,8 @@ struct fit_ctx {
     void* xchg_user = nullptr;
     HBuf<uint8_t> h_x;               // staging for the host exchange
     DBuf<uint64_t> xcount;           // per-rank counters (component-sharded stats)
+    bool force_coll = false;         // FIT_FLAG_COLLECTIVES: sharded path + exchange at world 1
+    bool collective() const { return world > 1 || force_coll; }
     bool persistent = true;          // one-launch work-queue engine (FIT_ENGINE=rounds: host loop)
     int cus = 256;
     DBuf<uint8_t> ectl, ering;
@@ -212,6 +214,7 @@ struct fit_ctx {
     DBuf<NodeRec> rec;
     DBuf<int32_t> col_cpu, col_mem, col_gpu, col_av, perm;
     DBuf<uint32_t> col_mask;
+    DBuf<int32_t> rb_cpu, rb_mem, rb_gpu;  // fit_read_nodes scratch (col_* stay the loaded table)
     std::vector<uint32_t> h_mask;
     bool have_nodes = false;
 
@@ -245,7 +248,7 @@ struct fit_ctx {
 
     ~fit_ctx() {
         for (auto* b : {&col_cpu, &col_mem, &col_gpu, &col_av, &perm, &jcpu, &jmem, &jgpu,
-                        &jwall, &out, &jl, &jpk})
+                        &jwall, &out, &jl, &jpk, &rb_cpu, &rb_mem, &rb_gpu})
             b->release();
         rec.release();
         tlhdr.release();
@@ -362,7 +365,7 @@ int alloc_cols(fit_ctx* c, int32_t n) {
 // ------------------------------------------------------------------------ exchange
 // In-place collectives on device buffers: RCCL over xGMI, or the caller's host exchange.
 int xchg(fit_ctx* c, int op, void* dbuf, int64_t count) {
-    if (c->world == 1 || count == 0) return 0;
+    if (!c->collective() || count == 0) return 0;
     if (!c->xchg) {
         switch (op) {
             case FIT_XCHG_ALLGATHER_U64: {
@@ -434,6 +437,14 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
+    // task ring: a committer publishes a round only after all of its previous round's tiles are
+    // done, so at most nc * job tiles * slices tiles are outstanding; the ring must hold them all
+    // (a granule overwritten before its worker read it would be lost)
+    int32_t max_slices = 1;
+    for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
+    if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)(engine_ring_bytes() / 8))
+        return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
+                    nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     size_t lds = engine_lds_bytes(maxnodes);
     // experiment knob: a larger LDS request caps the blocks per CU (e.g. > 80 KB: one per CU)
     if (const char* e = getenv("FIT_ENGINE_LDS_MIN")) lds = std::max(lds, (size_t)atol(e));
@@ -535,7 +546,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     // or by nodes (north_star: every rank scans 1/world of every component, RCCL each round)
     int mode = 0;
     std::vector<char> owned(C, 1);
-    if (c->world > 1) {
+    if (c->collective()) {
         mode = c->shard_mode;
         if (mode == FIT_SHARD_AUTO) mode = C >= c->world ? FIT_SHARD_COMPONENTS : FIT_SHARD_NODES;
         if (mode == FIT_SHARD_COMPONENTS) {
@@ -726,6 +737,14 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
+    {  // task ring capacity (see run_persistent)
+        int32_t max_slices = 1;
+        for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
+        if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices >
+            (int64_t)(engine_ring_bytes() / 8))
+            return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
+                        nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
+    }
     const size_t lds = engine_tl_lds_bytes(maxnodes);
     const int per_cu = engine_tl_blocks_per_cu(lds);
     if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine_tl does not fit on a CU (lds %zu)", lds);
@@ -792,7 +811,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     std::vector<int32_t> jb;
     int rc = build_job_lists(c, J, S, jb);
     if (rc) return rc;
-    const bool node_sharded = c->world > 1;
+    const bool node_sharded = c->collective();
     const int shards = c->world, srank = c->rank;
     S.shard_mode = node_sharded ? FIT_SHARD_NODES : 0;
     S.components = C;
@@ -999,6 +1018,7 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (const char* ev = getenv("FIT_ENGINE")) c->persistent = strcmp(ev, "rounds") != 0;
     c->rank = o.rank;
     c->world = o.world;
+    c->force_coll = (o.flags & FIT_FLAG_COLLECTIVES) != 0;
     c->shard_mode = o.shard_mode;
     c->xchg = o.exchange;
     c->xchg_user = o.exchange_user;
@@ -1013,7 +1033,14 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) rc = FIT_E_HIP;
     for (auto& e : c->ev)
         if (!rc && hipEventCreate(&e) != hipSuccess) rc = FIT_E_HIP;
-    if (!rc && c->world > 1 && !c->xchg) {
+    if (!rc && c->world == 1 && c->force_coll && !c->xchg) {
+        // FIT_FLAG_COLLECTIVES: a one-rank RCCL communicator, so the sharded code path and its
+        // RCCL calls run on one GPU exactly as they do in a multi-GPU group
+        ncclUniqueId id;
+        ncclResult_t r = ncclGetUniqueId(&id);
+        if (r == ncclSuccess) r = ncclCommInitRank(&c->comm, 1, id, 0);
+        if (r != ncclSuccess) rc = fail(FIT_E_RCCL, "ncclCommInitRank(1 rank): %s", ncclGetErrorString(r));
+    } else if (!rc && c->world > 1 && !c->xchg) {
         if (!o.nccl_id) {
             rc = fail(FIT_E_INVAL, "world > 1 needs nccl_id");
         } else {
@@ -1046,6 +1073,9 @@ int fit_load_nodes(fit_ctx* c, int32_t n, const int32_t* cpu, const int32_t* mem
     if (!c) return fail(FIT_E_INVAL, "null ctx");
     if (n < 0 || n > FIT_MAX_NODES || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
         return fail(FIT_E_INVAL, "bad node arrays");
+    // the columns are overwritten below: until the load succeeds there is no valid node table
+    // (a failed load must not leave new offsets paired with old node rows)
+    c->have_nodes = c->have_tl = false;
     HIP_TRY(hipSetDevice(c->device));
     if (alloc_cols(c, n)) return FIT_E_OOM;
     const size_t b = sizeof(int32_t) * n;
@@ -1063,6 +1093,7 @@ int fit_load_nodes_device(fit_ctx* c, int32_t n, const int32_t* cpu, const int32
     if (!c) return fail(FIT_E_INVAL, "null ctx");
     if (n < 0 || n > FIT_MAX_NODES || (n > 0 && (!cpu || !mem || !gpu || !av || !mask)))
         return fail(FIT_E_INVAL, "bad node arrays");
+    c->have_nodes = c->have_tl = false;  // see fit_load_nodes
     HIP_TRY(hipSetDevice(c->device));
     if (alloc_cols(c, n)) return FIT_E_OOM;
     const size_t b = sizeof(int32_t) * n;
@@ -1112,10 +1143,7 @@ int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, con
     int rc = check_place_args(c, j, cpu, mem, gpu, wall, part, kmax, out);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (int32_t q = 0; q < j; ++q)
-        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0 ||
-            (nk && std::max<int>(nk[q], 1) > kmax))
-            return fail(FIT_E_INVAL, "job %d: negative demand or nodes_k > kmax", q);
+    // demands >= 0 and nodes_k <= kmax are checked on the device (k_prefilter): FIT_E_INVAL
     size_t m = std::max(j, 1);
     if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
         c->jpart.ensure(m) || c->jk.ensure(m) || c->out.ensure(m * kmax))
@@ -1154,12 +1182,18 @@ int fit_read_nodes(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
     if (!c->have_nodes) return fail(FIT_E_STATE, "fit_load_nodes not called");
     if (c->n > 0 && (!cpu || !mem || !gpu)) return fail(FIT_E_INVAL, "null output");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(launch_scatter_nodes(c->st, c->rec.p, c->nn, c->col_cpu.p, c->col_mem.p,
-                                 c->col_gpu.p));
+    // scatter into scratch columns seeded with the loaded table: col_* must keep the table of
+    // the last fit_load_nodes (fit_load_timeline builds slot 0 from it), whatever was queried
     const size_t b = sizeof(int32_t) * c->n;
-    HIP_TRY(hipMemcpyAsync(cpu, c->col_cpu.p, b, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipMemcpyAsync(mem, c->col_mem.p, b, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipMemcpyAsync(gpu, c->col_gpu.p, b, hipMemcpyDeviceToHost, c->st));
+    const size_t m = std::max<int32_t>(c->n, 1);
+    if (c->rb_cpu.ensure(m) || c->rb_mem.ensure(m) || c->rb_gpu.ensure(m)) return FIT_E_OOM;
+    HIP_TRY(hipMemcpyAsync(c->rb_cpu.p, c->col_cpu.p, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->rb_mem.p, c->col_mem.p, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(c->rb_gpu.p, c->col_gpu.p, b, hipMemcpyDeviceToDevice, c->st));
+    HIP_TRY(launch_scatter_nodes(c->st, c->rec.p, c->nn, c->rb_cpu.p, c->rb_mem.p, c->rb_gpu.p));
+    HIP_TRY(hipMemcpyAsync(cpu, c->rb_cpu.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(mem, c->rb_mem.p, b, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(gpu, c->rb_gpu.p, b, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return 0;
 }
@@ -1259,9 +1293,7 @@ int fit_place_tl(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem,
     int rc = check_place_tl_args(c, j, cpu, mem, gpu, wall, part, out_node, out_start);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (int32_t q = 0; q < j; ++q)
-        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0)
-            return fail(FIT_E_INVAL, "job %d: negative demand", q);
+    // demands >= 0 are checked on the device (k_prefilter): FIT_E_INVAL
     size_t m = std::max(j, 1);
     if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
         c->jpart.ensure(m) || c->out.ensure(m) || c->outs.ensure(m))

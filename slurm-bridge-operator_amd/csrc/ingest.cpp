@@ -452,12 +452,19 @@ int64_t gres_gpus(sv v) {
 }
 
 // A node takes new work unless a State token says otherwise (DOWN*, IDLE+DRAIN, ...); the flags
-// follow `scontrol show node` (base state + '+'-joined flags, '*' = not responding).
+// follow `scontrol show node` (base state + '+'-joined flags, '*' = not responding).  The short
+// suffixes of sinfo-style states stand for the same flags as their long '+' forms, so IDLE~ and
+// IDLE+POWERED_DOWN decide alike: ~ POWERED_DOWN, % POWERING_DOWN, ! POWER_DOWN (pending),
+// $ MAINT, @ REBOOT_REQUESTED, ^ REBOOT_ISSUED refuse new work; # POWERING_UP and - PLANNED
+// do not.
 bool state_schedulable(sv v) {
     if (v.empty()) return true;
     if (v.find('*') != sv::npos) return false;  // not responding
     for (sv tok : split(v, "+")) {
-        while (!tok.empty() && strchr("~#!%$@^-", tok.back())) tok.remove_suffix(1);
+        while (!tok.empty() && strchr("~#!%$@^-", tok.back())) {
+            if (strchr("~!%$@^", tok.back())) return false;
+            tok.remove_suffix(1);
+        }
         static const char* const bad[] = {"DOWN",     "DRAIN",         "DRAINED",      "DRAINING",
                                           "FAIL",     "FAILING",       "FUTURE",       "MAINT",
                                           "POWERED_DOWN", "POWER_DOWN", "POWERING_DOWN",

@@ -24,7 +24,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (FIT_E_PARSE, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS,
+from ._lib import (FIT_E_PARSE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS,
                    FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32,
                    FIT_XCHG_MIN_U64, XCHG_FN, FitError, FitJobResources, FitNode, FitOpts, FitResources,
                    FitStats, check, lib)
@@ -35,6 +35,7 @@ __all__ = [
     "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
     "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
     "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS", "expand_hostlist", "ingest_nodes",
+    "FIT_FLAG_COLLECTIVES",
 ]
 
 
@@ -261,11 +262,11 @@ class Engine:
 
     def __init__(self, device: int = -1, rank: int = 0, world: int = 1, nccl_id: bytes | None = None,
                  window_min: int = 0, window_max: int = 0, shard_mode: int = 0,
-                 exchange: "TorchHostExchange | None" = None):
+                 exchange: "TorchHostExchange | None" = None, flags: int = 0):
         self._idbuf = C.create_string_buffer(nccl_id, 128) if nccl_id else None
         self._xchg = exchange
         o = FitOpts(device, rank, world, C.cast(self._idbuf, C.c_void_p) if self._idbuf else None,
-                    shard_mode, window_min, window_max, 0, exchange.fn if exchange else XCHG_FN(), None)
+                    shard_mode, window_min, window_max, flags, exchange.fn if exchange else XCHG_FN(), None)
         h = C.c_void_p()
         check(lib().fit_create(C.byref(o), C.byref(h)), "fit_create")
         self._h = h
@@ -306,12 +307,16 @@ class Engine:
         check(lib().fit_load_partitions(self._h, len(cols[0]), *[_ptr(c) for c in cols]),
               "fit_load_partitions")
 
-    def place(self, jobs, kmax: int = 1):
+    def place(self, jobs, kmax: int = 1, out=None):
+        """Host arrays in, placements out[J, kmax] (an int32 array the caller may pass, e.g. pinned)."""
         cols = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
         part = np.ascontiguousarray(jobs.part, np.uint16)
         k = np.ascontiguousarray(jobs.nodes_k, np.uint16)
         j = len(part)
-        out = np.empty((j, kmax), np.int32)
+        if out is None:
+            out = np.empty((j, kmax), np.int32)
+        elif out.dtype != np.int32 or out.size != j * kmax or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous int32 array of J * kmax entries")
         st = FitStats()
         check(lib().fit_place(self._h, j, *[_ptr(c) for c in cols], _ptr(part), _ptr(k), kmax, _ptr(out),
                               C.byref(st)), "fit_place")
@@ -341,12 +346,16 @@ class Engine:
                                              *[_ptr(t) for t in (slot, cpu, mem, gpu)]), "fit_load_timeline_device")
         self.slots = int(slots)
 
-    def place_tl(self, jobs):
-        """Returns (node[J], start_slot[J], stats)."""
+    def place_tl(self, jobs, node=None, start=None):
+        """Returns (node[J], start_slot[J], stats); node / start may be caller int32 arrays."""
         cols = [np.ascontiguousarray(a, np.int32) for a in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)]
         part = np.ascontiguousarray(jobs.part, np.uint16)
         j = len(part)
-        node, start = np.empty(j, np.int32), np.empty(j, np.int32)
+        node = np.empty(j, np.int32) if node is None else node
+        start = np.empty(j, np.int32) if start is None else start
+        for a in (node, start):
+            if a.dtype != np.int32 or a.size != j or not a.flags.c_contiguous:
+                raise ValueError("node / start must be contiguous int32 arrays of J entries")
         st = FitStats()
         check(lib().fit_place_tl(self._h, j, *[_ptr(c) for c in cols], _ptr(part), _ptr(node), _ptr(start),
                                  C.byref(st)), "fit_place_tl")

@@ -40,6 +40,7 @@ EXPORTS = [
 XCHG_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64)
 FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MIN_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32 = 1, 2, 3, 4
 FIT_SHARD_AUTO, FIT_SHARD_NODES, FIT_SHARD_COMPONENTS = 0, 1, 2
+FIT_FLAG_COLLECTIVES = 1  # fit_opts.flags: multi-rank code path at world 1 (include/fitgpu.h)
 
 
 class FitOpts(C.Structure):

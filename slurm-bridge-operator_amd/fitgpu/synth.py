@@ -3,7 +3,7 @@
 The reference has no benchmark inputs; BASELINE.json names five configurations and
 SURVEY.md §8(d) fixes their distributions.  Every value here is a pure function of
 (seed, stream, index), so any slice of the stream can be generated independently (numpy here,
-a C twin in ``oracle/gen.c`` that must agree byte-for-byte — ``tests/test_synth.py``).
+a C twin of ``rnd``, ``ref_rnd`` in ``oracle/fitref.c:563``, that must agree bit-for-bit — ``tests/test_synth.py``).
 
     rnd(seed, stream, i) = mix64(seed + GOLDEN * (i * 64 + stream + 1))      (mod 2**64)
     uni(r, m)            = ((r >> 32) * m) >> 32                              in [0, m)
@@ -29,6 +29,7 @@ S_NCLASS, S_NMEM, S_NGPU, S_ACPU, S_AMEM, S_AGPU, S_NPART, S_AVF, S_AVV = range(
 S_RN, S_RS = 9, 10  # C5: running jobs per node, their release slots
 S_JCPU, S_JMEM, S_JGPUF, S_JGPUV, S_JWO, S_JWV, S_JPART, S_JK = range(16, 24)
 S_PTIME = 32
+S_JALL = 24  # c3o: job targets the all-nodes partition
 
 NODE_CPUS = np.array([32, 64, 96, 128, 192, 256], dtype=np.int64)
 NODE_MEMMUL = np.array([2048, 4096, 8192], dtype=np.int64)
@@ -211,7 +212,11 @@ CONFIGS = {
     "c3": (100_000, 1_000_000, 16, False, False),
     "c4": (100_000, 1_000_000, 16, True, True),
     "c5": (100_000, 1_000_000, 16, False, False),  # + 1,024-slot horizon (make_c5)
+    # C3 with overlapping partitions: every node also belongs to an all-nodes
+    # partition 16 that ~10 % of the jobs target, so the 16 partitions union into ONE component
+    "c3o": (100_000, 1_000_000, 16, False, False),
 }
+C3O_ALL_PCT = 10
 C5_SLOTS, C5_SLOT_MIN = 1024, 5  # 1,024 slots × 5 min = 85.3 h ≥ the longest walltime (2,880 min)
 
 
@@ -220,11 +225,17 @@ def make_config(name: str, nodes: int | None = None, jobs: int | None = None, sh
     ``shard`` s > 0 draws the s-th disjoint slice of the same streams (nodes [s*n, (s+1)*n), jobs
     [s*j, (s+1)*j)): an independent cluster of the same shape, for weak-scaling runs."""
     n, j, p, gh, mn = CONFIGS[name]
-    seed = SEEDS[name]
+    seed = SEEDS["c3" if name == "c3o" else name]
     n = n if nodes is None else nodes
     j = j if jobs is None else jobs
-    return (gen_nodes(seed, n, p, gh, start=shard * n), gen_jobs(seed, j, p, mn, start=shard * j),
-            gen_partitions(seed, p))
+    nd, jb = gen_nodes(seed, n, p, gh, start=shard * n), gen_jobs(seed, j, p, mn, start=shard * j)
+    if name != "c3o":
+        return nd, jb, gen_partitions(seed, p)
+    # c3o: C3's cluster and stream, plus partition p (all nodes) for C3O_ALL_PCT % of the jobs
+    nd.part_mask = nd.part_mask | np.uint32(1 << p)
+    i = np.arange(shard * j, shard * j + j, dtype=np.uint64)
+    jb.part = np.where(uni(rnd(seed, S_JALL, i), 100) < C3O_ALL_PCT, p, jb.part).astype(np.uint16)
+    return nd, jb, gen_partitions(seed, p + 1)
 
 
 def make_c5(nodes: int | None = None, jobs: int | None = None, shard: int = 0):

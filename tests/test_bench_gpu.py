@@ -1,5 +1,5 @@
 """bench.py keeps the driver's contract: one JSON line with the required keys, the roofline and
-CPU-baseline objects, for the C3 headline and the C5 workload; N>1 weak scaling rehearsed with two
+CPU-baseline objects, for the C3 headline, the C5 and c3o workloads; N>1 weak scaling rehearsed with two
 ranks on one GPU (gloo for the timing collectives)."""
 import json
 import os
@@ -24,13 +24,16 @@ def run(args, env=None, timeout=240):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("workload", ["c3", "c5"])
+@pytest.mark.parametrize("workload", ["c3", "c5", "c3o"])
 def test_bench_line(workload):
-    d = run(["bench.py", "--workload", workload, "--steps", "1", "--warmup", "1", "--cpu-sample", "200"])
-    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
+    d = run(["bench.py", "--workload", workload, "--steps", "1", "--warmup", "1", "--cpu-scale", "0.01"])
+    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["value"] > 0 and d["kernel_path_value"] > 0
     assert set(d["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
-    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and {v["kind"] for v in cb["variants"]} == {"naive-port", "component-aware",
+                                                                          "multicore"}
     assert d["config"]["workload"] == workload and d["config"]["jobs"] == 1_000_000
+    assert d["placed_plus_unplaced_per_s"] <= d["value"]
 
 
 def test_bench_two_rank_rehearsal():
@@ -38,6 +41,6 @@ def test_bench_two_rank_rehearsal():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     d = run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-             "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse"])
+             "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse", "--scaling", "weak"])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["config"]["jobs"] == 2_000_000 and d["config"]["per_gpu"]["jobs"] == 1_000_000

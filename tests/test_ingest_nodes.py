@@ -55,7 +55,10 @@ def test_gres_forms():
                                       ("IDLE+CLOUD", True), ("COMPLETING", True), ("DOWN", False),
                                       ("IDLE*", False), ("IDLE+DRAIN", False), ("DRAINED", False),
                                       ("ALLOCATED+DRAINING", False), ("MAINT", False),
-                                      ("IDLE+POWERED_DOWN", False), ("FUTURE", False), ("IDLE~", True)])
+                                      ("IDLE+POWERED_DOWN", False), ("FUTURE", False), ("IDLE~", False),
+                                      ("IDLE%", False), ("IDLE+POWERING_DOWN", False), ("MIXED#", True),
+                                      ("IDLE+POWERING_UP", True), ("IDLE$", False), ("MIXED@", False),
+                                      ("IDLE-", True)])
 def test_state(state, ok):
     t = f"NodeName=n CPUTot=4 CPUAlloc=0 RealMemory=10 AllocMem=0 State={state} Partitions=p"
     nodes, _ = ingest_nodes(t, ["p"])

@@ -48,6 +48,17 @@ def test_c3_prefix():
     check_parity(nodes, jobs, parts)
 
 
+@pytest.mark.parametrize("engine", ["persistent", "rounds"])
+def test_c3o_overlapping_partitions_prefix(engine, monkeypatch):
+    """C3 plus an all-nodes partition (~10 % of the jobs): the 17 partitions union into ONE
+    component, so a single serial chain decides every job."""
+    if engine == "rounds":
+        monkeypatch.setenv("FIT_ENGINE", "rounds")
+    nodes, jobs, parts = synth.make_config("c3o", 20000, 100000)
+    st = check_parity(nodes, jobs, parts)
+    assert st["components"] == 1
+
+
 @pytest.mark.parametrize("wmin,wmax", [(1, 1), (1, 8), (64, 64), (512, 65536)])
 def test_window_policies_c2(wmin, wmax):
     nodes, jobs, parts = synth.make_config("c2", 512, 8192)
