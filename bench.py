@@ -304,20 +304,27 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
         m = max(1, min(int(m * scale), jobs.j))
         return m, synth.Jobs(*(x[:m] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part, jobs.nodes_k)))
 
+    # samples sized by an evaluation budget (each variant ~2-6 s on the box): a job costs one
+    # evaluation per node it scans — every node (naive) or its component's (the others)
+    ncomp = _components(nodes.part_mask)
+    per_comp = nodes.n / max(ncomp, 1)
+    par = min(threads, ncomp)
+    budget = 2e8 if tline is not None else 2e9
+    m_naive, m_comp, m_mc = budget / nodes.n, 3 * budget / per_comp, 3 * budget * par / per_comp
     if tline is not None:
-        runs = [("naive-port", 1, 2000, lambda s: po.ref_place_tl(nodes, tline, s, parts)[2],
+        runs = [("naive-port", 1, m_naive, lambda s: po.ref_place_tl(nodes, tline, s, parts)[2],
                  "oracle/fitref_tl.c ref_place_tl (SPEC §2b, dense timelines, every node per job)"),
-                ("component-aware", 1, 6000, lambda s: po.cpu_place_tl(nodes, tline, s, parts, 1)[2],
+                ("component-aware", 1, m_comp, lambda s: po.cpu_place_tl(nodes, tline, s, parts, 1)[2],
                  "oracle/cpu_baseline.c cpu_place_tl (own component's nodes only)"),
-                ("multicore", threads, 60000, lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads)[2],
-                 f"oracle/cpu_baseline.c cpu_place_tl, components on {threads} threads")]
+                ("multicore", threads, m_mc, lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads)[2],
+                 f"oracle/cpu_baseline.c cpu_place_tl, {ncomp} components on {threads} threads")]
     else:
-        runs = [("naive-port", 1, 20000, lambda s: po.ref_place(nodes, s, parts)[1],
+        runs = [("naive-port", 1, m_naive, lambda s: po.ref_place(nodes, s, parts)[1],
                  "oracle/fitref.c ref_place (C restatement of the scalar sequential path, every node per job)"),
-                ("component-aware", 1, 200000, lambda s: po.cpu_place(nodes, s, parts, 1)[1],
+                ("component-aware", 1, m_comp, lambda s: po.cpu_place(nodes, s, parts, 1)[1],
                  "oracle/cpu_baseline.c cpu_place (own component's nodes only, vectorised scan)"),
-                ("multicore", threads, 1_000_000, lambda s: po.cpu_place(nodes, s, parts, threads)[1],
-                 f"oracle/cpu_baseline.c cpu_place, components on {threads} threads")]
+                ("multicore", threads, m_mc, lambda s: po.cpu_place(nodes, s, parts, threads)[1],
+                 f"oracle/cpu_baseline.c cpu_place, {ncomp} components on {threads} threads")]
     variants = []
     for kind, cores, m, fn, what in runs:
         m, sub = prefix(m)
@@ -331,6 +338,25 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
     return {"value": best["value"], "unit": "placements/s", "cores": best["cores"], "kind": "port",
             "variant": best["kind"], "sample": best["sample"], "host_cpu": _cpu_model(),
             "variants": variants}
+
+
+def _components(mask) -> int:
+    """Partition components (partitions joined by nodes in several of them), as the engine forms them."""
+    par = list(range(32))
+
+    def find(x):
+        while par[x] != x:
+            par[x] = par[par[x]]
+            x = par[x]
+        return x
+    used = set()
+    for m in np.unique(mask):
+        bits = [b for b in range(32) if (int(m) >> b) & 1]
+        used.update(bits)
+        for b in bits[1:]:
+            ra, rb = find(bits[0]), find(b)
+            par[max(ra, rb)] = min(ra, rb)
+    return len({find(b) for b in used})
 
 
 def _cpu_model() -> str:

@@ -15,11 +15,12 @@ __global__ __launch_bounds__(64) void k_dec_bench(int w, int32_t* out, unsigned 
             S->rec[r].h = MwHdr{0u, 0, MW_M, r, 1, 1, 0, 0, 1u, 0u, KEY_INF};
         }
         if (lane < MW_M) {
-            const uint64_t key = ((uint64_t)(lane + 1) << 32) | (uint32_t)(r * MW_M + lane);
-            S->rec[r].it[lane] = MwItem{key, r * MW_M + lane, r * MW_M + lane, 1000000, 1000000, 0, 0, 1u, 0, 0, 0};
+            S->rec[r].it[lane] = MwItem{(uint32_t)(r * MW_M + lane), (uint32_t)(lane + 1), r * MW_M + lane,
+                                        r * MW_M + lane, 1000000, 1000000, 0, 0, 1u, 0u, 0u, 0u};
         }
     }
     for (int i = lane; i < 64; i += 64) S->bitmap[i] = 0u;
+    if (lane == 0) S->dn = 0ull;
     __syncthreads();
     CompPlan P{};
     P.nb = 0;
@@ -46,6 +47,9 @@ extern "C" int dec_bench(int w, unsigned long long* host_out) {
     hipLaunchKernelGGL(fitgpu::k_dec_bench, dim3(1), dim3(64), lds, 0, w, out, cyc);
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     hipMemcpy(host_out, cyc, 32, hipMemcpyDeviceToHost);
+#ifdef MW_SEGSTAMP
+    hipMemcpyFromSymbol(host_out + 4, HIP_SYMBOL(fitgpu::g_seg), 64);
+#endif
     hipFree(out);
     hipFree(cyc);
     return 0;

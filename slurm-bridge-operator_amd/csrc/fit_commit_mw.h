@@ -6,18 +6,36 @@
 // state for job t (v >= t - (MW_M - 1), enforced by the helper).  The helper records the MW_M
 // smallest keys <= B among (clean candidates of t) ∪ (dirty rows), each item tagged clean (with
 // its node row) or dirty (its slot).  When the decider reaches t, only the nodes written by jobs
-// [v, t) — at most MW_M - 1 of them, the decider's own last decisions — can differ from the
-// snapshot.  It drops every listed item whose node is among them (a clean node since marked in
-// the bitmap, a dirty slot whose version is >= v) and re-evaluates those nodes at their current
-// state.  If the list held MW_M items, at least one survives and every unlisted node has a key
-// above it; if it held fewer, it held every candidate <= B.  Either way
-//     best = min(surviving items, re-evaluated nodes)
+// [v, t) — at most MW_M - 1 of them, the decider's own last decisions, kept in its "written
+// ring" — can differ from the snapshot.  It drops every item whose node is in the live part of
+// the ring and evaluates the live ring rows at their current state.  If the list held MW_M items,
+// at least one survives and every unlisted node has a key above it; if it held fewer, it held
+// every candidate <= B.  Either way
+//     best = min(surviving items, live ring rows)
 // is the sequential answer restricted to keys <= B, and the SPEC stop rule reduces to
-// "best > B with B finite" (a clean candidate is always <= B).  No fallback path exists.
+// "best > B with B finite" (a clean candidate is always <= B).  The argument needs nothing of a
+// row or bitmap word the helper read after the snapshot: any node changed after v is in the live
+// ring, so a torn or newer read of it only produces an item the decider drops.
 //
-// LDS protocol (one workgroup): DS instructions of a wave execute in issue order, so plain
-// stores followed by a flag store are seen in that order by a wave that read the flag first;
-// the fences below are compiler barriers only.
+// Cost model (measured on gfx950, tools/ubench: one wave alone) — what shapes the code below:
+// a dependent VALU op ≈ 4.7 cycles, any scalar branch ≈ 25-30, a VALU → SGPR → SALU hand-off
+// ≈ 20-36, v_readlane → v_writelane ≈ 8.6, one LDS round trip ≈ 50-64.  So the decider's job
+// step is straight-line VALU with ONE exception branch per job (record not ready, B exceeded,
+// dirty set full, end of window), the written ring lives in lanes 0..7 (slot = job & 7, a
+// compile-time lane in the 8-way unrolled loop), item staleness is a lane-parallel XOR against
+// the ring rotated with DPP row_ror, the minimum over ring rows and items is three 64-bit DPP
+// steps over 8 lanes, and the next job's record is read while this one is decided.  The
+// decision's bookkeeping (dirty row, bitmap bit, placement) is issued by the decider itself as
+// fire-and-forget LDS writes.
+//
+// LDS protocol (one workgroup), C++ memory model at workgroup scope on LDS ("local"):
+//   decider → helpers: dirty rows, bitmap, then {decided, nu} by a release store;
+//   helpers: relaxed poll of {decided, nu}, then an acquire fence, then rows / bitmap.
+//   helper → decider: record items and header, then the record's ready word by a release store;
+//   decider: relaxed load of the ready word, an acquire fence, then the record's data.
+// On gfx950 (no threadgroup split) a workgroup-scope release / acquire on LDS is an
+// `s_waitcnt lgkmcnt(0)` before the store / after the load (checked in the ISA); both sit where
+// the counter is already drained, so the protocol costs no cycles on the decider's chain.
 #pragma once
 #include "fit_common.h"
 
@@ -28,31 +46,20 @@ namespace fitgpu {
 #endif
 constexpr int MW_M = MW_ITEMS;          // items per pre-resolved record (> snapshot lag)
 constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once job t-8 is decided
-constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider [+ 1 recorder] + MW_H helpers
-// MW_RECORDER: wave 1 is the RECORDER — it takes the decider's decisions from a small LDS queue
-// and does their bookkeeping (dirty row, bitmap, placement, the {decided, nu} publish), which
-// leaves the decider's serial chain with the decision itself.  0: the decider does both.
-#ifndef MW_RECORDER
-#ifdef MW_DECIDER_BENCH
-#define MW_RECORDER 0
-#else
-#define MW_RECORDER 1
+constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
+#ifndef MW_IDLE4
+#define MW_IDLE4 0  // 1: wave 4 (the decider's SIMD partner) stays idle, six helpers
 #endif
-#endif
-#ifndef MW_HELPERS
-#define MW_HELPERS (MW_RECORDER ? 6 : 7)
-#endif
-constexpr int MW_H = MW_HELPERS;  // waves 1 + MW_RECORDER .. MW_RECORDER + MW_H
-static_assert(MW_H + 1 + MW_RECORDER <= MW_WAVES, "one wave per role");
-constexpr int MW_DQ = 16;         // decision queue (decider -> recorder)
+constexpr int MW_H = MW_WAVES - 1 - MW_IDLE4;  // helpers: waves 1..7 (but 4 with MW_IDLE4)
+static_assert(MW_M == 8, "the decider holds one item per lane of its 8-lane ring group");
+static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
 constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
-#define MW_HSLEEP 2
+#define MW_HSLEEP 12  // helper back-off per missing decided job, in units of 64 cycles
 #endif
 constexpr int MW_EPL = (MAX_SLICES * KS + 63) / 64;  // candidate entries per helper lane
 static_assert(MW_EPL <= 2, "at most two candidate entries per lane");
-static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
 struct alignas(16) MwRow {  // dirty row, current state
     int32_t cpu, mem, gpu, avail;
@@ -60,16 +67,15 @@ struct alignas(16) MwRow {  // dirty row, current state
     int32_t orig, ver;  // ver: last job (window index) that created or changed it
 };
 
-struct alignas(16) MwItem {
-    uint64_t key;
-    int32_t tag;   // >= 0 dirty slot; -1 clean candidate (row below)
-    int32_t orig;
+struct alignas(16) MwItem {  // 48 B; the decider reads the first 36
+    uint32_t pos, score;  // key = score << 32 | pos
+    int32_t tag, orig;    // tag: dirty slot (>= 0) or -1 (a clean candidate; row below)
     int32_t cpu, mem, gpu, avail;
     uint32_t mask, pad0, pad1, pad2;
 };
 
 struct alignas(16) MwHdr {
-    uint32_t ready;  // t + 1 once the record of job t is complete
+    uint32_t ready;  // t + 1 once the record of job t is complete (release store, last)
     int32_t v, n, q;
     int32_t cpu, mem, gpu, wall;
     uint32_t pbit, pad;
@@ -82,15 +88,15 @@ struct alignas(16) MwRec {
 };
 
 struct alignas(16) MwShared {
-    uint32_t decided;  // jobs resolved by the decider
-    uint32_t nu;       // dirty rows (stored together with decided)
-    uint32_t halt;     // decider stopped early
+    uint64_t dn;       // {decided (low 32), nu (high 32)}: the helpers' snapshot, release-stored
+    uint32_t halt;     // decider stopped
     uint32_t fail;     // helper / decider watchdog
     int32_t res[4];    // CommitResult of the window
     uint32_t pad[8];
     MwRec rec[MW_R];
-    uint4 dq[MW_DQ];  // decision of job t in dq[t % MW_DQ]: {t + 1, winner, slot, 0}
     MwRow rows[UCAP];
+    MwRow sink_rows[64];   // targets of the decider's lanes that do not write a dirty row
+    uint32_t sink_words[64];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
 };
 
@@ -99,12 +105,11 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 }
 
 #ifdef FIT_STAMPS
-// [comp][0] decider cycles, [1] decider wait-for-record, [2] decided jobs,
+// [comp][0] decider cycles, [1] decider waiting for records (slow path), [2] decided jobs,
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
-// [7] decider check+reduce, [8] decider decide+publish, [9] waits of each round's first jobs,
+// [7] (unused), [8] (unused), [9] decider waits in each round's first 8 jobs,
 // [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record,
-// [15] helper snapshot → extraction start, [16] decider: records not ready at the first read,
-// [17] recorder cycles, [18] recorder waiting for decisions, [19] recorder jobs
+// [15] helper snapshot → extraction start, [16] decider: records not ready at the first read
 constexpr int MW_NSTAMP = 24;
 __device__ unsigned long long g_mw[64][MW_NSTAMP];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -118,13 +123,15 @@ __device__ unsigned long long g_mw[64][MW_NSTAMP];
 #define MW_ADD(I_, V_)
 #endif
 
+// ---- LDS hand-off primitives (workgroup scope, LDS only) ------------------------------------
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void cbar() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
 
 // Tile readiness: the window's scan tiles complete while the window is being
 // committed; a helper waits for the (job tile)'s per-tile counter to reach nslice before reading
@@ -227,9 +234,140 @@ __device__ __forceinline__ uint64_t mw_key(int32_t cf, int32_t mf, int32_t gf, i
     return ok ? (((uint64_t)sc << 32) | pos) : KEY_INF;
 }
 
+// ---- DPP building blocks ---------------------------------------------------------------------
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    if constexpr (ROWMASK == 0xf)  // every lane has a source: a plain DPP move
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+    else  // lanes of rows outside the mask keep their value
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+// one 64-bit min step against the DPP-permuted value (2 moves, a 64-bit compare, 2 selects)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint64_t dpp_min64(uint64_t v) {
+    const uint32_t lo = dpp32<CTRL, ROWMASK>((uint32_t)v), hi = dpp32<CTRL, ROWMASK>((uint32_t)(v >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    return o < v ? o : v;
+}
+// minimum over each group of 8 lanes, in all 8 of them: quad swaps, then the half-row mirror
+__device__ __forceinline__ uint64_t min8_64(uint64_t v) {
+    v = dpp_min64<0xb1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_min64<0x4e>(v);   // quad_perm [2,3,0,1]
+    return dpp_min64<0x141>(v);  // row_half_mirror
+}
+// Fused DPP ALU ops in inline asm (hipcc emits a DPP move plus the ALU op for the builtins).
+// Each string opens with the two wait states a DPP read of a VGPR written by the previous VALU
+// instruction needs (cdna_hip_programming.md: DPP hazard; `s_nop 1`).
+#define MW_DPP_MIN(v, CTL) asm volatile("s_nop 1\n\tv_min_u32_dpp %0, %0, %0 " CTL : "+v"(v))
+__device__ __forceinline__ uint32_t dppmin_qp1032(uint32_t v) { MW_DPP_MIN(v, "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"); return v; }
+__device__ __forceinline__ uint32_t dppmin_qp2301(uint32_t v) { MW_DPP_MIN(v, "quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"); return v; }
+__device__ __forceinline__ uint32_t dppmin_hmirror(uint32_t v) { MW_DPP_MIN(v, "row_half_mirror row_mask:0xf bank_mask:0xf"); return v; }
+__device__ __forceinline__ uint32_t dppmin_mirror(uint32_t v) { MW_DPP_MIN(v, "row_mirror row_mask:0xf bank_mask:0xf"); return v; }
+__device__ __forceinline__ uint32_t dppmin_bcast15(uint32_t v) { MW_DPP_MIN(v, "row_bcast:15 row_mask:0xa bank_mask:0xf"); return v; }
+__device__ __forceinline__ uint32_t dppmin_bcast31(uint32_t v) { MW_DPP_MIN(v, "row_bcast:31 row_mask:0xc bank_mask:0xf"); return v; }
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_min32(uint32_t v) {
+    if constexpr (CTRL == 0xb1) return dppmin_qp1032(v);
+    else if constexpr (CTRL == 0x4e) return dppmin_qp2301(v);
+    else if constexpr (CTRL == 0x141) return dppmin_hmirror(v);
+    else if constexpr (CTRL == 0x140) return dppmin_mirror(v);
+    else if constexpr (CTRL == 0x142) return dppmin_bcast15(v);
+    else return dppmin_bcast31(v);
+}
+// d = src ^ (x rotated by K within its row of 16 lanes); NOP: src of the DPP just written
+template <int K, bool NOP>
+__device__ __forceinline__ uint32_t dpp_ror_xor(uint32_t x, uint32_t y) {
+    uint32_t d;
+    if constexpr (NOP)
+        asm volatile("s_nop 1\n\tv_xor_b32_dpp %0, %1, %2 row_ror:%3 row_mask:0xf bank_mask:0xf"
+                     : "=v"(d) : "v"(x), "v"(y), "i"(K));
+    else
+        asm volatile("v_xor_b32_dpp %0, %1, %2 row_ror:%3 row_mask:0xf bank_mask:0xf"
+                     : "=v"(d) : "v"(x), "v"(y), "i"(K));
+    return d;
+}
+// 64-bit minimum over each group of 8 lanes, in all 8: the 32-bit minimum of the high words,
+// then of the low words among the lanes holding it (fused DPP mins, no 64-bit compares)
+__device__ __forceinline__ uint64_t min8_2pass(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    uint32_t mh = dpp_min32<0xb1>(hi);
+    mh = dpp_min32<0x4e>(mh);
+    mh = dpp_min32<0x141>(mh);
+    uint32_t ml = hi == mh ? lo : 0xffffffffu;
+    ml = dpp_min32<0xb1>(ml);
+    ml = dpp_min32<0x4e>(ml);
+    ml = dpp_min32<0x141>(ml);
+    return ((uint64_t)mh << 32) | ml;
+}
+// 32-bit minimum over the wave, valid in lane 63
+__device__ __forceinline__ uint32_t wave_min32_l63(uint32_t v) {
+    v = dpp_min32<0xb1>(v);
+    v = dpp_min32<0x4e>(v);
+    v = dpp_min32<0x141>(v);
+    v = dpp_min32<0x140>(v);
+    v = dpp_min32<0x142, 0xa>(v);
+    return dpp_min32<0x143, 0xc>(v);
+}
+// 64-bit minimum over the wave (uniform): two 32-bit passes
+__device__ __forceinline__ uint64_t wave_min64_2pass(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t mh = (uint32_t)__builtin_amdgcn_readlane((int)wave_min32_l63(hi), 63);
+    const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane(
+        (int)wave_min32_l63(hi == mh ? lo : 0xffffffffu), 63);
+    return ((uint64_t)mh << 32) | ml;
+}
+// minimum over the wave, valid in lane 63
+__device__ __forceinline__ uint64_t wave_min64_l63(uint64_t v) {
+    v = dpp_min64<0xb1>(v);
+    v = dpp_min64<0x4e>(v);
+    v = dpp_min64<0x141>(v);       // row_half_mirror: 8-lane groups
+    v = dpp_min64<0x140>(v);       // row_mirror: whole rows of 16
+    v = dpp_min64<0x142, 0xa>(v);  // row_bcast:15 → rows 1 and 3
+    return dpp_min64<0x143, 0xc>(v);  // row_bcast:31 → rows 2 and 3
+}
+
+// v_writelane_b32: lane `l` of `old` := SGPR `x` (no clang builtin on this toolchain)
+__device__ __forceinline__ int32_t writelane(int32_t x, int l, int32_t old) {
+    int32_t r;
+    // the lane select goes through M0 (one SGPR operand per VALU instruction on gfx9)
+    asm("v_writelane_b32 %0, %1, m0" : "=v"(r) : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(l), "0"(old));
+    return r;
+}
+template <int L>
+__device__ __forceinline__ int32_t writelane_c(int32_t x, int32_t old) {  // compile-time lane
+    int32_t r;
+    asm("v_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(__builtin_amdgcn_readfirstlane(x)), "i"(L), "0"(old));
+    return r;
+}
+__device__ __forceinline__ int32_t readlane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// Wait until job tt's scan tile is complete (uniform; `ready` = tiles known complete, they finish
+// roughly in order).  false: the decider halted / a watchdog tripped.
+__device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& ready, MwShared* S) {
+    if (!T.tdone) return true;
+    const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
+    if (tile < ready) return true;
+    for (unsigned sp = 0;; ++sp) {
+        if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+            T.need)
+            break;
+        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
+        if (sp > MW_SPIN_LIMIT) {
+            lds_st(&S->fail, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ready = tile + 1;
+    return true;
+}
+
+// ------------------------------------------------------------------------------- helper
 // Helper entry lists: MW_EPL clean candidates + UPL dirty rows per lane, each key tagged with
 // its entry index in the low bits (positions < 2^29, FIT_MAX_NODES), INF stays INF.
-constexpr int MW_NE = MW_EPL + UPL;
+constexpr int UPL_MW = UCAP / 64;
+constexpr int MW_NE = MW_EPL + UPL_MW;
 static_assert(MW_NE <= 8, "entry index takes 3 bits (and 4 bits of item index each in 32)");
 static_assert(MW_M <= 15, "item index + 1 fits 4 bits");
 __device__ __forceinline__ uint64_t mw_tag(uint64_t k, int e) {
@@ -259,32 +397,9 @@ __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
     }
 }
 
-// Wait until job tt's scan tile is complete (uniform; `ready` = tiles known complete, they finish
-// roughly in order).  false: the decider halted / a watchdog tripped.
-__device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& ready, MwShared* S) {
-    if (!T.tdone) return true;
-    const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
-    if (tile < ready) return true;
-    for (unsigned sp = 0;; ++sp) {
-        if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-            T.need)
-            break;
-        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if (sp > MW_SPIN_LIMIT) {
-            lds_st(&S->fail, 1u);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    ready = tile + 1;
-    return true;
-}
-
-// ------------------------------------------------------------------------------- helper
-// Helper h (1..MW_H) pre-resolves jobs t = h-1, h-1+MW_H, ...  Loads run two jobs ahead (keys,
-// job row, bound) and one job ahead (the node rows of the candidates); the three register sets
-// are indexed by literal constants only (3-way unrolled loop).
+// Helper h (1..MW_H) pre-resolves jobs t = h-1, h-1+H, ...  Loads run two jobs ahead (keys, job
+// row, bound) and one job ahead (the node rows of the candidates); the three register sets are
+// indexed by literal constants only (3-way unrolled loop).
 #define MW_HSTEP(A, B_, C)                                                                     \
     {                                                                                          \
         if (t >= P.w) goto hdone;                                                              \
@@ -312,28 +427,32 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
             jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
             jbd[C] = bnd[P.slot0 + tt_];                                                       \
         }                                                                                      \
-        /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs */                  \
-        uint32_t v_;                                                                           \
+        /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs (and so has read  \
+           record slot t & 7's previous job) */                                                \
+        uint64_t dn_;                                                                          \
         MW_CLK(hw0_);                                                                          \
         for (unsigned sp_ = 0;; ++sp_) {                                                       \
-            v_ = lds_ld(&S->decided);                                                          \
-            if ((int)v_ + (MW_M - 1) >= t) break;                                              \
-            if (lds_ld(&S->halt) | lds_ld(&S->fail)) goto hdone;                               \
+            dn_ = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
+            const int lag_ = t - (MW_M - 1) - rfl((int32_t)(uint32_t)dn_);                     \
+            if (lag_ <= 0) break;                                                              \
+            if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
             if (sp_ > MW_SPIN_LIMIT) {                                                         \
                 lds_st(&S->fail, 1u);                                                          \
                 goto hdone;                                                                    \
             }                                                                                  \
-            __builtin_amdgcn_s_sleep(MW_HSLEEP); /* keep the LDS free for the decider */       \
+            /* the decider needs ~1k cycles a job: sleep about that long per missing job      \
+               instead of polling (every poll is an LDS access the decider queues behind) */   \
+            for (int s_ = min(lag_, 8); s_ > 0; --s_) __builtin_amdgcn_s_sleep(MW_HSLEEP);     \
         }                                                                                      \
-        /* the snapshot's row / bitmap reads are issued after the flag read that admitted it */ \
-        asm volatile("" ::: "memory");                                                         \
+        lds_acquire(); /* the rows / bitmap the decider released with dn_ */                   \
+        const uint32_t v_ = (uint32_t)rfl((int32_t)(uint32_t)dn_);                             \
+        const int nu_ = rfl((int32_t)(uint32_t)(dn_ >> 32));                                   \
         {                                                                                      \
             MW_CLK(hw1_);                                                                      \
             MW_ACC(a_hw, hw1_ - hw0_);                                                         \
             MW_ACC(a_hp, -(long long)hw1_);                                                    \
             MW_ACC(a_hx, -(long long)hw1_);                                                    \
         }                                                                                      \
-        const int nu_ = (int)lds_ld(&S->nu);                                                   \
         const JobRec& J_ = jr[A];                                                              \
         const uint64_t Bd_ = jbd[A];                                                           \
         uint64_t x0[MW_EPL];                                                                   \
@@ -344,12 +463,13 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
             const bool dirty_ = (S->bitmap[rel_ >> 5] >> (rel_ & 31)) & 1u;                    \
             x0[e] = ok_ && !dirty_ ? k_ : KEY_INF;                                             \
         }                                                                                      \
-        uint64_t xd[UPL];                                                                      \
-        MwRow wr_[UPL];                                                                        \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) {                                      \
+        uint64_t xd[UPL_MW];                                                                   \
+        MwRow wr_[UPL_MW];                                                                     \
+        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) {                                   \
             xd[i] = KEY_INF;                                                                   \
+            wr_[i] = MwRow{0, 0, 0, 0, 0u, 0u, 0, 0};                                          \
             const int u_ = i * 64 + lane;                                                      \
-            if (i * 64 < nu_) {                                                                \
+            if (i * 64 < nu_) { /* uniform: rows [0, nu) exist */                              \
                 wr_[i] = S->rows[u_ < nu_ ? u_ : 0];                                           \
                 const uint64_t y_ = mw_key(wr_[i].cpu, wr_[i].mem, wr_[i].gpu, wr_[i].avail,   \
                                            wr_[i].mask, wr_[i].pos, J_.cpu, J_.mem, J_.gpu,    \
@@ -365,44 +485,53 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         }                                                                                      \
         /* every entry tagged with its index (pos << 3 | e keeps the order of distinct nodes) and\
            sorted per lane once; each extraction is then one wave minimum over the lane heads  \
-           plus a predicated shift in the winning lane, and the items are written in one pass */\
+           plus a predicated shift in the winning lane */                                      \
         uint64_t q_[MW_NE];                                                                    \
         _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) q_[e] = mw_tag(x0[e], e);           \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) q_[MW_EPL + i] = mw_tag(xd[i], MW_EPL + i);\
+        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) q_[MW_EPL + i] = mw_tag(xd[i], MW_EPL + i);\
         mw_sort(q_);                                                                           \
-        /* item index + 1 of each entry, 4 bits per entry (0: not taken) */                    \
+        /* item index + 1 of each entry, 4 bits per entry (0: not taken); depth = entries this  \
+           lane gave (a prefix of its sorted list) */                                          \
         uint32_t sel_ = 0u;                                                                    \
+        int depth_ = 0;                                                                        \
         /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */  \
-        const int nmax_ = rfl(min(MW_M, t - (int)v_ + 1));                                     \
+        const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
         for (; n_ < nmax_; ++n_) {                                                             \
-            int wl_;                                                                           \
-            const uint64_t best_ = wave_min_key_lane(q_[0], wl_);                              \
+            const uint64_t best_ = wave_min64_2pass(q_[0]);                                    \
             if (best_ == KEY_INF) break;                                                       \
-            const bool me_ = lane == wl_;                                                      \
+            const bool me_ = q_[0] == best_; /* tagged keys are unique */                      \
             const uint32_t sv_ = (uint32_t)(n_ + 1) << (4u * ((uint32_t)best_ & 7u));          \
             sel_ = me_ ? sel_ | sv_ : sel_;                                                    \
+            depth_ += me_;                                                                     \
             _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
                 q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
             q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
         }                                                                                      \
-        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) if ((sel_ >> (4 * e)) & 15u)        \
-            R_->it[((sel_ >> (4 * e)) & 15u) - 1u] = MwItem{x0[e], -1, ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e],\
-                                     rk[A][e], 0, 0, 0};                                       \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) if ((sel_ >> (4 * (MW_EPL + i))) & 15u) \
-            R_->it[((sel_ >> (4 * (MW_EPL + i))) & 15u) - 1u] = MwItem{xd[i], i * 64 + lane, wr_[i].orig, wr_[i].cpu,   \
-                                              wr_[i].mem, wr_[i].gpu, wr_[i].avail, wr_[i].mask,\
-                                              0, 0, 0};                                        \
+        /* items: the lanes that gave an entry store it (exec-masked: only those lanes use   \
+           the LDS, which the decider shares) */                                               \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) {                                   \
+            const uint32_t ix_ = (sel_ >> (4 * e)) & 15u;                                      \
+            if (ix_)                                                                           \
+                R_->it[ix_ - 1u] = MwItem{(uint32_t)x0[e], (uint32_t)(x0[e] >> 32), -1,        \
+                                          ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e],    \
+                                          rk[A][e], 0u, 0u, 0u};                               \
+        }                                                                                      \
+        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) {                                   \
+            const uint32_t ix_ = (sel_ >> (4 * (MW_EPL + i))) & 15u;                           \
+            if (ix_)                                                                           \
+                R_->it[ix_ - 1u] = MwItem{(uint32_t)xd[i], (uint32_t)(xd[i] >> 32),            \
+                                          i * 64 + lane, wr_[i].orig, wr_[i].cpu, wr_[i].mem,  \
+                                          wr_[i].gpu, wr_[i].avail, wr_[i].mask, 0u, 0u, 0u};  \
+        }                                                                                      \
         if (lane == 0) {                                                                       \
-            R_->h.cpu = J_.cpu;                                                                \
-            R_->h.mem = J_.mem;                                                                \
-            R_->h.gpu = J_.gpu;                                                                \
-            R_->h.wall = J_.wall;                                                              \
-            R_->h.pbit = J_.pbit;                                                              \
-            R_->h.B = Bd_;                                                                     \
-            cbar();                                                                            \
-            /* {ready, v, n, q}: one 16-byte store, after everything else of the record */     \
-            *reinterpret_cast<uint4*>(&R_->h) =                                                \
-                make_uint4((uint32_t)t + 1u, v_, (uint32_t)n_, (uint32_t)J_.q);                 \
+            *reinterpret_cast<v4i32*>(&R_->h.cpu) = v4i32{J_.cpu, J_.mem, J_.gpu, J_.wall};    \
+            *reinterpret_cast<uint4*>(&R_->h.pbit) =                                           \
+                make_uint4(J_.pbit, 0u, (uint32_t)Bd_, (uint32_t)(Bd_ >> 32));                 \
+            R_->h.v = (int32_t)v_;                                                             \
+            R_->h.n = n_;                                                                      \
+            R_->h.q = J_.q;                                                                    \
+            lds_release(); /* items and header before the ready word */                        \
+            lds_st(&R_->h.ready, (uint32_t)t + 1u);                                            \
         }                                                                                      \
         {                                                                                      \
             MW_CLK(hp1_);                                                                      \
@@ -414,10 +543,10 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
     }
 
 __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
-                                          const NodeRec* __restrict__ rec_,
-                                          const uint64_t* __restrict__ cand_,
-                                          const uint64_t* __restrict__ bnd_,
-                                          const JobRec* __restrict__ wjob_, int h, MwTiles T) {
+                                       const NodeRec* __restrict__ rec_,
+                                       const uint64_t* __restrict__ cand_,
+                                       const uint64_t* __restrict__ bnd_,
+                                       const JobRec* __restrict__ wjob_, int h, MwTiles T) {
     const GAS NodeRec* const rec = gview(rec_);
     const GAS uint64_t* const cand = gview(cand_);
     const GAS uint64_t* const bnd = gview(bnd_);
@@ -490,81 +619,232 @@ hdone:;
 #undef MW_HSTEP
 
 // ------------------------------------------------------------------------------ decider
-// The "written ring": lane l (and every lane l + 8k) holds the row the decider wrote for the
-// last job j ≡ l (mod 8): job index, slot and the row's current fields.  For job t an entry is
-// live iff its job >= v (the record's snapshot); live entries are exactly the nodes that may
-// differ from the snapshot, so they are re-evaluated and every record item on one of their
-// positions is dropped.  When a slot is written again its older entry dies (job = -1), so a live
-// entry always holds the slot's current row.  All decision work is VALU on lanes 0..7; the only
-// LDS round trip per job is the record read.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_rot(uint32_t v) {  // within a 16-lane row, all valid
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
-}
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_min8(uint32_t v) { return min(v, dpp_rot<CTRL>(v)); }
+// One wave; lanes 0..7 carry the "written ring" (the decisions of the last 8 jobs: job t's entry
+// in lane t & 7 — its node's position and row as that job left it, its dirty slot, the job) and
+// record t's items (lane i: item i).  A ring entry is live for job t iff its job >= the record's
+// snapshot v; when a node is written again its older entry dies, so a live entry always holds
+// the node's current row.
+struct MwRing {
+    v4i32 a;       // cpu, mem, gpu, avail   (= MwRow's first 16 B)
+    v4i32 b;       // mask, pos, orig, job   (= MwRow's last 16 B; job -1: dead)
+    int32_t slot;  // dirty slot
+};
 
-// min over lanes 0..7 (valid in every one of them): quad swaps, then half-row mirror
-__device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
-    v = dpp_min8<0xb1>(v);   // quad_perm [1,0,3,2]
-    v = dpp_min8<0x4e>(v);   // quad_perm [2,3,0,1]
-    v = dpp_min8<0x141>(v);  // row_half_mirror
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-}
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+struct MwRecRegs {  // one record as this lane sees it: header (every lane) and item lane & 7
+    v4u32 h0, h1, h2;  // {ready, v, n, q}, {cpu, mem, gpu, wall}, {pbit, -, B lo, B hi}
+    v4u32 i0, i1;      // {pos, score, tag, orig}, {cpu, mem, gpu, avail}
+    uint32_t i2;       // mask
+};
 
-// v_writelane_b32: lane `l` of `old` := SGPR `x` (no clang builtin on this toolchain).  The lane
-// select goes through M0 (one SGPR operand per VALU instruction on gfx9).
-__device__ __forceinline__ int32_t writelane(int32_t x, int l, int32_t old) {
-    int32_t r;
-    // readfirstlane: a value the compiler believes divergent would otherwise get a VGPR here
-    asm("v_writelane_b32 %0, %1, m0"
-        : "=v"(r)
-        : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(l), "0"(old));
-    return r;
-}
-__device__ __forceinline__ uint32_t writelane(uint32_t x, int l, uint32_t old) {
-    return (uint32_t)writelane((int32_t)x, l, (int32_t)old);
-}
+struct MwDec {
+    int t, nu, placed, stop;
+    bool exit;  // the window is finished (end, stop or watchdog): later steps change nothing
+#ifdef MW_SEGSTAMP
+    unsigned long long seg[8], prev;
+#endif
+};
+// diagnostic (decbench only): cycles per segment of a decider step, s_memtime at each point
+#ifdef MW_SEGSTAMP
+__device__ unsigned long long g_seg[8];
+#define MW_SEG(D_, i)                                                                           \
+    do {                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        unsigned long long now_;                                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");            \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        if (i > 0) D_.seg[i] += now_ - D_.prev;                                                 \
+        D_.prev = now_;                                                                         \
+    } while (0)
+#else
+#define MW_SEG(D_, i)
+#endif
 
-// bit 8i of the result is set iff byte i of m is nonzero
-__device__ __forceinline__ uint64_t any_in_byte(uint64_t m) {
-    m |= m >> 4;
-    m |= m >> 2;
-    m |= m >> 1;
-    return m & 0x0101010101010101ull;
+__device__ __forceinline__ const __attribute__((address_space(3))) v4u32* lds4(const void* p) {
+    return (const __attribute__((address_space(3))) v4u32*)(uintptr_t)p;
 }
-
-// one lane's view of a record: the header (every lane) and item i8 (lanes 8 i8 + r)
-__device__ __forceinline__ void mw_read_rec(const MwRec* R, int i8, uint4& h0, uint4& h1,
-                                            uint4& h2, uint4& i0, uint4& i1, uint4& i2) {
-    // {ready, v, n, q} is one 16-byte LDS store on the helper side (its last); read first
-    const uint4* hp = reinterpret_cast<const uint4*>(&R->h);
-    const uint4* ip = reinterpret_cast<const uint4*>(&R->it[i8]);
-    h0 = hp[0];
-    // plain LDS loads may be issued in any order: keep the flag word's read first (the wave's
-    // DS instructions then execute in issue order, after the helper's record stores it saw)
-    asm volatile("" ::: "memory");
-    h1 = hp[1];
-    h2 = hp[2];
-    i0 = ip[0];
-    i1 = ip[1];
-    i2 = ip[2];
+__device__ __forceinline__ void mw_read_rec(const MwRec* R, int i8, MwRecRegs& x) {
+    const __attribute__((address_space(3))) v4u32* hp = lds4(&R->h);
+    const __attribute__((address_space(3))) v4u32* ip = lds4(&R->it[i8]);
+    x.h0 = hp[0];
+    x.h1 = hp[1];
+    x.h2 = hp[2];
+    x.i0 = ip[0];
+    x.i1 = ip[1];
+    x.i2 = ((const __attribute__((address_space(3))) uint32_t*)ip)[8];
 }
 
-constexpr uint32_t MW_DQ_END = 0xfffffffeu;  // queue entry kind: the decider stopped here
+// One job of the decider: job D.t with record `cur` (its data read after an acquire of the ready
+// word `flag`; refreshed in place on the slow path), `nxt` receives record t+1.  E = t & 7 is a
+// compile-time constant.  Straight-line: the decision is computed unconditionally and selected (no
+// exec-masked region), its bookkeeping is masked with `go` instead of branched around, and the
+// only branch is the rare exception (record not ready, B exceeded, dirty set full).  Once D.exit
+// is set the step has no effect: the caller tests it once per 8 jobs.
+template <int E>
+__device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec& D, MwRing& R,
+                                          MwRecRegs& cur, MwRecRegs& nxt, uint32_t& flag,
+                                          int32_t& oq, int32_t& ov, int32_t* out, int kmax,
+                                          uint64_t& waitcyc) {
+    const int lane = threadIdx.x & 63;
+    const int t = D.t;
+    if (t >= P.w) D.exit = true;
+    MW_SEG(D, 0);
+    // publish the decisions so far (the previous job's row / bitmap writes were issued before
+    // record t's reads, all of which are complete here): release store of {decided, nu}
+    lds_release();
+    __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    // ready word of record t+1 (relaxed; acquired below, before its data is read)
+    const MwRec* Rn = &S->rec[(t + 1) & (MW_R - 1)];
+    const uint32_t flag_n = lds_ld(&Rn->h.ready);
+    MW_SEG(D, 1);
 
-// Wait until the recorder has published job t - MW_DQ (queue entry t % MW_DQ is free).
-// false: the watchdog tripped (the failure flag is set).
-__device__ __forceinline__ bool mw_dq_space(MwShared* S, int t, int& dseen) {
-    for (unsigned sp = 0;; ++sp) {
-        dseen = rfl((int)lds_ld(&S->decided));
-        if (t < dseen + MW_DQ) return true;
-        if (sp > MW_SPIN_LIMIT || rfl((int)lds_ld(&S->fail))) {
-            lds_st(&S->fail, 1u);
-            return false;
+    // the decision of job t against record `x`
+    struct Dec {
+        uint64_t bs;  // best key (uniform)
+        int32_t sc, sm, sg, sa, sk, so, ss;  // per lane: its candidate's row, demand subtracted
+        int w, wslot;
+        bool placed, fresh, stopB, full;
+    };
+    auto decide = [&](const MwRecRegs& x) {
+        Dec d;
+        const int32_t v = (int32_t)x.h0.y, n = (int32_t)x.h0.z;
+        const int32_t jc = (int32_t)x.h1.x, jm = (int32_t)x.h1.y, jg = (int32_t)x.h1.z,
+                      jw = (int32_t)x.h1.w;
+        const uint32_t jp = x.h2.x;
+        const uint64_t B = ((uint64_t)x.h2.w << 32) | x.h2.z;
+        // live ring rows at their current state
+        const bool live = R.b.w >= v;
+        const uint64_t rk0 = mw_key(R.a.x, R.a.y, R.a.z, R.a.w, (uint32_t)R.b.x, (uint32_t)R.b.y,
+                                    jc, jm, jg, jw, jp);
+        const uint64_t rkey = live ? rk0 : KEY_INF;
+        // item staleness: its node is in the live ring.  Lanes 8..15 take a copy of the ring
+        // (row_ror:8), so row_ror:k, k = 0..7, shows lane i < 8 every ring entry once.
+        const uint32_t P0 = live ? (uint32_t)R.b.y : 0xffffffffu;  // positions are < 2^29
+        const uint32_t P8 = dpp32<0x128>(P0);
+        const uint32_t P2 = (lane & 8) ? P8 : P0;
+        const uint32_t ip = x.i0.x;
+        const uint32_t d0 = ip ^ P2, d1 = dpp_ror_xor<1, true>(P2, ip),
+                       d2 = dpp_ror_xor<2, false>(P2, ip), d3 = dpp_ror_xor<3, false>(P2, ip),
+                       d4 = dpp_ror_xor<4, false>(P2, ip), d5 = dpp_ror_xor<5, false>(P2, ip),
+                       d6 = dpp_ror_xor<6, false>(P2, ip), d7 = dpp_ror_xor<7, false>(P2, ip);
+        const uint32_t dmin = min(min(min(d0, d1), min(d2, d3)), min(min(d4, d5), min(d6, d7)));
+        const uint64_t ik0 = ((uint64_t)x.i0.y << 32) | ip;
+        const uint64_t ikey = (lane < n && dmin != 0u) ? ik0 : KEY_INF;
+        const bool tr = rkey < ikey;  // this lane's ring row beats its item
+        const uint64_t cand = tr ? rkey : ikey;
+        // the winner's fields, demand already subtracted (selected per lane, read from one)
+        d.sc = (tr ? R.a.x : (int32_t)x.i1.x) - jc;
+        d.sm = (tr ? R.a.y : (int32_t)x.i1.y) - jm;
+        d.sg = (tr ? R.a.z : (int32_t)x.i1.z) - jg;
+        d.sa = tr ? R.a.w : (int32_t)x.i1.w;
+        d.sk = tr ? R.b.x : (int32_t)x.i2;
+        d.so = tr ? R.b.z : (int32_t)x.i0.w;
+        d.ss = tr ? R.slot : (int32_t)x.i0.z;
+        const uint64_t best = min8_2pass(cand);
+        // lanes 0..7 all hold `best`; the winner is the lane whose candidate equals it
+        const uint64_t mine = __ballot(cand == best) & 0xffull;
+        d.w = __builtin_ctzll(mine | 0x100ull) & 7;
+        const uint32_t bhi = (uint32_t)readlane((int32_t)(best >> 32), 0);
+        const uint32_t blo = (uint32_t)readlane((int32_t)(uint32_t)best, 0);
+        d.bs = ((uint64_t)bhi << 32) | blo;
+        d.placed = d.bs != KEY_INF;
+        d.wslot = readlane(d.ss, d.w);
+        d.fresh = d.placed && d.wslot < 0;
+        d.full = d.fresh && D.nu >= UCAP;
+        d.stopB = B != KEY_INF && d.bs > B;
+        return d;
+    };
+    Dec d = decide(cur);
+    MW_SEG(D, 2);
+#ifdef MW_DECIDER_BENCH
+    const bool rec_missing = false;  // diagnostic: records pre-filled, never "not ready"
+#else
+    const bool rec_missing = flag != (uint32_t)t + 1u;
+#endif
+    if (__builtin_expect(!D.exit && (rec_missing || d.stopB || d.full), 0)) {  // the one branch
+        if (rec_missing) {  // record t not complete when read: wait for it, read it again
+            MW_CLK(c0);
+            for (unsigned sp = 0;; ++sp) {
+                flag = lds_ld(&S->rec[t & (MW_R - 1)].h.ready);
+                if (flag == (uint32_t)t + 1u) break;
+                if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
+                    lds_st(&S->fail, 1u);
+                    D.stop = 3;
+                    D.exit = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(0);
+            }
+            lds_acquire();
+            mw_read_rec(&S->rec[t & (MW_R - 1)], lane & 7, cur);
+            {
+                MW_CLK(c1);
+                MW_ACC(waitcyc, c1 - c0);
+            }
+            d = decide(cur);
         }
-        __builtin_amdgcn_s_sleep(0);
+        if (!D.exit && (d.stopB || d.full)) {
+            D.stop = d.stopB ? 1 : 2;  // candidate list exhausted (rescan) / dirty set full
+            D.exit = true;
+        }
     }
+    // ---- apply job t (masked by `go`; the ring is not read again once D.exit is set) ----------
+    MW_SEG(D, 3);
+    const bool go = !D.exit;
+    const bool placed = d.placed && go, fresh = d.fresh && go;
+    const int w = d.w;
+    const int32_t pos = (int32_t)(uint32_t)d.bs;
+    const int32_t nc = readlane(d.sc, w), nm = readlane(d.sm, w), ng = readlane(d.sg, w);
+    const int32_t na = readlane(d.sa, w), nk = readlane(d.sk, w), no = readlane(d.so, w);
+    const int32_t slot = fresh ? D.nu : d.wslot;
+    // an older ring entry of the same node dies (lane E is rewritten below)
+    R.b.w = (placed && R.b.y == pos) ? -1 : R.b.w;
+    R.a.x = writelane_c<E>(nc, R.a.x);
+    R.a.y = writelane_c<E>(nm, R.a.y);
+    R.a.z = writelane_c<E>(ng, R.a.z);
+    R.a.w = writelane_c<E>(na, R.a.w);
+    R.b.x = writelane_c<E>(nk, R.b.x);
+    R.b.y = writelane_c<E>(pos, R.b.y);
+    R.b.z = writelane_c<E>(no, R.b.z);
+    R.b.w = writelane_c<E>(placed ? t : -1, R.b.w);
+    R.slot = writelane_c<E>(slot, R.slot);
+    MW_SEG(D, 4);
+    // read record t+1's data after acquiring its ready word (the load above is long done)
+    flag = flag_n;
+    lds_acquire();
+    mw_read_rec(Rn, lane & 7, nxt);
+    MW_SEG(D, 5);
+    // bookkeeping: dirty row, bitmap bit — fire-and-forget LDS writes from lane E (the other
+    // lanes write their own sink words: no exec masking, no branch)
+    {
+        const bool me = lane == E && placed;
+        MwRow* dst = me ? &S->rows[slot] : &S->sink_rows[lane];
+        __attribute__((address_space(3))) v4i32* d4 = (__attribute__((address_space(3))) v4i32*)(uintptr_t)dst;
+#ifndef MW_DBG_NOROWS
+        d4[0] = R.a;
+        d4[1] = R.b;
+#endif
+        const uint32_t rel = (uint32_t)pos - (uint32_t)P.nb;
+        const bool setb = me && fresh;
+        uint32_t* bw = setb ? &S->bitmap[rel >> 5] : &S->sink_words[lane];
+#ifndef MW_DBG_NOBITMAP
+        __hip_atomic_fetch_or(bw, setb ? 1u << (rel & 31) : 0u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+    }
+    D.nu += fresh;
+    D.placed += placed;
+    MW_SEG(D, 6);
+    // placement of job t parked in lane t & 63 (after an exit that lane is past the last store)
+    oq = writelane(rfl((int32_t)cur.h0.w), t & 63, oq);
+    ov = writelane(placed ? no : -1, t & 63, ov);
+    if (E == 7 && go && (t & 63) == 63) {  // uniform, once per 64 jobs: store 64 placements
+        if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;
+        oq = -1;
+    }
+    D.t = t + (go ? 1 : 0);
+    MW_SEG(D, 7);
 }
 
 // Out of line (as is mw_helper): called once per round, each gets its own register allocation
@@ -574,287 +854,72 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     const CompPlan P = plan_sgpr(Pref);  // by value (see mw_helper)
     MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
-    const int r8 = lane & 7;   // ring entry this lane holds (full row in lanes 0..7 only)
-    const int i8 = lane >> 3;  // record item this lane reads: lane 8i + r tests item i vs entry r
-    const uint32_t nb = (uint32_t)P.nb;
 #ifndef MW_NO_SETPRIO
-    __builtin_amdgcn_s_setprio(3);  // shares its SIMD with helper wave 4
+    __builtin_amdgcn_s_setprio(3);  // shares its SIMD with a helper wave
 #endif
-    int nu = 0, placed = 0, stop = 0, t = 0;
-    int32_t wj = -1, ws = -1, wc = 0, wm = 0, wg = 0, wa = 0, wo = -1;  // written ring
-    uint32_t wk = 0, wp = ~0u;
+    MwDec D{0, 0, 0, 0, false};
+#ifdef MW_SEGSTAMP
+    for (int i = 0; i < 8; ++i) D.seg[i] = 0;
+    D.prev = 0;
+#endif
+    MwRing R;
+    R.a = v4i32{0, 0, 0, 0};
+    R.b = v4i32{0, -1, -1, -1};  // dead, position matching no item
+    R.slot = -1;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
-    int dseen = 0;             // jobs the recorder has published (last seen)
-    MW_DECL(a_nr);
-    MW_DECL(a_dw);
-    MW_DECL(a_d0);  // waits of the round's first MW_R jobs (pipeline fill)
-    MW_DECL(a_dc);
-    MW_DECL(a_dd);
+    uint64_t waitcyc = 0;
     MW_CLK(d0);
-    for (; t < P.w; ++t) {
-        MW_CLK(dw0);
-        uint4 h0, h1, h2, i0, i1, i2;
-        for (unsigned sp = 0;; ++sp) {  // speculative: header and items in one round trip
-            mw_read_rec(&S->rec[t & (MW_R - 1)], i8, h0, h1, h2, i0, i1, i2);
+    // record 0: wait for its ready word, acquire, read
+    MwRecRegs ra, rb;
+    uint32_t flag = 0;
+    if (P.w > 0) {
+        for (unsigned sp = 0;; ++sp) {
+            flag = lds_ld(&S->rec[0].h.ready);
 #ifdef MW_DECIDER_BENCH
-            if (true) break;  // diagnostic: records pre-filled, no helpers
+            break;
 #endif
-            if ((uint32_t)rfl((int32_t)h0.x) == (uint32_t)t + 1u) break;
-            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {  // uniform exit
+            if (flag == 1u) break;
+            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                 lds_st(&S->fail, 1u);
-                stop = 3;
+                D.stop = 3;
+                D.exit = true;
                 break;
             }
-            MW_ACC(a_nr, sp == 0);
             __builtin_amdgcn_s_sleep(0);
         }
-        const MwHdr h{h0.x, (int32_t)h0.y, (int32_t)h0.z, (int32_t)h0.w, (int32_t)h1.x,
-                      (int32_t)h1.y, (int32_t)h1.z, (int32_t)h1.w, h2.x, h2.y,
-                      ((uint64_t)h2.w << 32) | h2.z};
-        const MwItem it{((uint64_t)i0.y << 32) | i0.x, (int32_t)i0.z, (int32_t)i0.w,
-                        (int32_t)i1.x, (int32_t)i1.y, (int32_t)i1.z, (int32_t)i1.w,
-                        i2.x, i2.y, i2.z, i2.w};
-        if (stop) break;
-        MW_CLK(dw1);
-        MW_ACC(a_dw, dw1 - dw0);
-        MW_ACC(a_d0, t < MW_R ? dw1 - dw0 : 0);
-        const int v = __builtin_amdgcn_readfirstlane(h.v);
-        const int n = __builtin_amdgcn_readfirstlane(h.n);
-        const bool live = wj >= v;
-        // first record item whose node no live ring entry touches (items are sorted by key)
-        const uint64_t tm = __ballot(live && (uint32_t)it.key == wp);
-        const uint64_t valid = n >= 8 ? ~0ull : (1ull << (8 * n)) - 1ull;
-        const uint64_t un = valid & 0x0101010101010101ull & ~any_in_byte(tm);
-        const int il = un ? __builtin_ctzll(un) : 0;  // its lane (8 i*)
-        uint64_t best = KEY_INF;
-        if (un)
-            best = ((uint64_t)__builtin_amdgcn_readlane((int)(it.key >> 32), il) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)it.key, il);
-        // live ring rows at their current state: any better than that item?
-        const uint64_t wk0 = mw_key(wc, wm, wg, wa, wk, wp, h.cpu, h.mem, h.gpu, h.wall, h.pbit);
-        const uint64_t wkey = live ? wk0 : KEY_INF;
-        const uint64_t bet = __ballot(wkey < best) & 0xffull;
-        int rl = -1;  // winning ring lane, -1: the item
-        if (bet) {
-            if (__popcll(bet) == 1) {
-                rl = __builtin_ctzll(bet);
-            } else {
-                const uint32_t mh = min8_u32((uint32_t)(wkey >> 32));
-                const uint32_t ml = min8_u32((uint32_t)(wkey >> 32) == mh ? (uint32_t)wkey : ~0u);
-                rl = __builtin_ctzll(__ballot((uint32_t)(wkey >> 32) == mh &&
-                                              (uint32_t)wkey == ml) & 0xffull);
-            }
-            best = ((uint64_t)__builtin_amdgcn_readlane((int)(wkey >> 32), rl) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wkey, rl);
-        }
-        MW_CLK(dw2);
-        MW_ACC(a_dc, dw2 - dw1);
-        if (__ballot(h.B != KEY_INF && best > h.B)) {  // uniform
-            stop = 1;  // candidate list exhausted: rescan next round
-            break;
-        }
-        int32_t node = -1;
-        int32_t dkind = -1, dslot = -1;  // winner for the recorder: item 0..7, 8 ring, -1 none
-        if (best != KEY_INF) {
-            int32_t sc, sm, sg, sa, slot;
-            uint32_t sk;
-            if (rl >= 0) {
-                sc = __builtin_amdgcn_readlane(wc, rl);
-                sm = __builtin_amdgcn_readlane(wm, rl);
-                sg = __builtin_amdgcn_readlane(wg, rl);
-                sa = __builtin_amdgcn_readlane(wa, rl);
-                sk = __builtin_amdgcn_readlane(wk, rl);
-                node = __builtin_amdgcn_readlane(wo, rl);
-                slot = __builtin_amdgcn_readlane(ws, rl);
-            } else {
-                sc = __builtin_amdgcn_readlane(it.cpu, il);
-                sm = __builtin_amdgcn_readlane(it.mem, il);
-                sg = __builtin_amdgcn_readlane(it.gpu, il);
-                sa = __builtin_amdgcn_readlane(it.avail, il);
-                sk = __builtin_amdgcn_readlane(it.mask, il);
-                node = __builtin_amdgcn_readlane(it.orig, il);
-                slot = __builtin_amdgcn_readlane(it.tag, il);
-            }
-            const bool fresh = slot < 0;  // a clean node becomes dirty row nu
-            if (fresh && nu == UCAP) {
-                stop = 2;  // dirty set full
-                break;
-            }
-            if (fresh) slot = nu++;
-            const int32_t nc = sc - __builtin_amdgcn_readfirstlane(h.cpu);
-            const int32_t nm = sm - __builtin_amdgcn_readfirstlane(h.mem);
-            const int32_t ng = sg - __builtin_amdgcn_readfirstlane(h.gpu);
-            const uint32_t pos = (uint32_t)best;
-            dkind = rl >= 0 ? 8 : il >> 3;
-            dslot = slot;
-            if (!MW_RECORDER && lane == 0) {
-                S->rows[slot] = MwRow{nc, nm, ng, sa, sk, pos, node, t};
-                if (fresh) {
-                    const uint32_t rel = pos - nb;
-                    __hip_atomic_fetch_or(&S->bitmap[rel >> 5], 1u << (rel & 31),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            // ring entry t & 7 (job, slot, pos in every lane; the row in lane t & 7 only); an
-            // older entry of the same slot dies
-            const int e = t & 7;
-            const bool me = r8 == e;
-            wj = me ? t : (ws == slot ? -1 : wj);
-            ws = me ? slot : ws;
-            wp = me ? pos : wp;
-            wc = writelane(nc, e, wc);
-            wm = writelane(nm, e, wm);
-            wg = writelane(ng, e, wg);
-            wa = writelane(sa, e, wa);
-            wk = writelane(sk, e, wk);
-            wo = writelane(node, e, wo);
-            ++placed;
-        }
-        if (MW_RECORDER) {
-            // queue entry t % MW_DQ is free once the recorder has published job t - MW_DQ
-            if (t >= dseen + MW_DQ && !mw_dq_space(S, t, dseen)) {
-                stop = 3;
-                break;
-            }
-            if (lane == 0)  // one 16-byte store: the recorder reads it with one load
-                *reinterpret_cast<uint4*>(&S->dq[t & (MW_DQ - 1)]) =
-                    make_uint4((uint32_t)t + 1u, (uint32_t)dkind, (uint32_t)dslot, 0u);
-        } else {
-            oq = writelane(__builtin_amdgcn_readfirstlane(h.q), t & 63, oq);
-            ov = writelane(node, t & 63, ov);
-            if ((t & 63) == 63) {  // uniform: flush 64 placements
-                if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // global: vmcnt only
-                oq = -1;
-            }
-            cbar();
-            if (lane == 0)  // {decided, nu} in one 8-byte LDS store
-                __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
-                                   ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        MW_CLK(dw3);
-        MW_ACC(a_dd, dw3 - dw2);
+        lds_acquire();
+        mw_read_rec(&S->rec[0], lane & 7, ra);
+    } else {
+        D.exit = true;
     }
-    if (MW_RECORDER) {  // end marker: the recorder finishes job t - 1 and reports `stop`
-        if (stop == 3 || t < dseen + MW_DQ || mw_dq_space(S, t, dseen)) {
-            if (lane == 0)
-                *reinterpret_cast<uint4*>(&S->dq[t & (MW_DQ - 1)]) =
-                    make_uint4((uint32_t)t + 1u, (uint32_t)MW_DQ_END, (uint32_t)stop, 0u);
-        }
-    } else if (oq >= 0 && lane < (t & 63)) {
-        ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
+    // 8-way unrolled: the ring lane (t & 7) is a constant in every step; the two record register
+    // sets alternate with the step's parity; the exit is tested once per 8 steps
+    while (!D.exit) {
+        mw_decide<0>(S, P, D, R, ra, rb, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<1>(S, P, D, R, rb, ra, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<2>(S, P, D, R, ra, rb, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<3>(S, P, D, R, rb, ra, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<4>(S, P, D, R, ra, rb, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<5>(S, P, D, R, rb, ra, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<6>(S, P, D, R, ra, rb, flag, oq, ov, out, kmax, waitcyc);
+        mw_decide<7>(S, P, D, R, rb, ra, flag, oq, ov, out, kmax, waitcyc);
     }
-    if (stop) lds_st(&S->halt, 1u);
+    const int t = D.t;
+    if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
+    // final {decided, nu}, then halt (the helpers' exit)
+    lds_release();
+    __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_st(&S->halt, 1u);
     MW_CLK(d1);
     MW_ADD(0, d1 - d0);
+#ifdef MW_SEGSTAMP
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) g_seg[i] = D.seg[i];
+#endif
+    MW_ADD(1, waitcyc);
     MW_ADD(2, t);
-    MW_ADD(1, a_dw);
-    MW_ADD(9, a_d0);
-    MW_ADD(7, a_dc);
-    MW_ADD(8, a_dd);
-    MW_ADD(16, a_nr);
-    return CommitResult{t, stop, nu, placed};
-}
-
-// ------------------------------------------------------------------------------ recorder
-// Takes the decisions in job order and does what the helpers and the output need: the dirty row
-// (current state, version t), the dirty bitmap bit of a fresh node, the placement (parked in lane
-// t & 63, stored 64 at a time), then {decided, nu} — the helpers' snapshot — in one 8-byte store
-// after the rest (DS order).  The winner's previous state comes from the record the decider used
-// (an item: its node did not change since the snapshot, or the decider would have dropped it) or
-// from the dirty row of a ring winner (this wave wrote it).  Record slot t % MW_R is reused only
-// for job t + MW_R, whose helper waits for decided >= t + 1: it is intact here.
-__device__ __noinline__ CommitResult mw_recorder(const CompPlan& Pref, MwShared* Sin,
-                                                 int32_t* __restrict__ out, int kmax) {
-    const CompPlan P = plan_sgpr(Pref);
-    MwShared* const S = lds_opaque(Sin);
-    const int lane = threadIdx.x & 63;
-    const uint32_t nb = (uint32_t)P.nb;
-    int nu = 0, placed = 0, stop = 0, t = 0;
-    int32_t oq = -1, ov = -1;
-    MW_DECL(a_rw);
-    MW_CLK(r0);
-    for (;; ++t) {
-        uint4 d;
-        MW_CLK(rw0);
-        for (unsigned sp = 0;; ++sp) {
-            asm volatile("" ::: "memory");  // a fresh LDS read every spin
-            d = *reinterpret_cast<const uint4*>(&S->dq[t & (MW_DQ - 1)]);
-            if ((uint32_t)rfl((int32_t)d.x) == (uint32_t)t + 1u) break;
-            if (sp > MW_SPIN_LIMIT || rfl((int32_t)lds_ld(&S->fail))) {
-                lds_st(&S->fail, 1u);
-                stop = 3;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(0);
-        }
-        if (stop) break;
-        {
-            MW_CLK(rw1);
-            MW_ACC(a_rw, rw1 - rw0);
-        }
-        const uint32_t kind = (uint32_t)rfl((int32_t)d.y);
-        if (kind == MW_DQ_END) {
-            stop = rfl((int32_t)d.z);
-            break;
-        }
-        asm volatile("" ::: "memory");  // record / row reads after the queue entry's read
-        const MwRec* R = &S->rec[t & (MW_R - 1)];
-        const uint4 hq = reinterpret_cast<const uint4*>(&R->h)[0];  // {ready, v, n, q}
-        int32_t node = -1;
-        if (kind != 0xffffffffu) {
-            const uint4 hd = reinterpret_cast<const uint4*>(&R->h)[1];  // {cpu, mem, gpu, wall}
-            const int slot = rfl((int32_t)d.z);
-            uint4 a, b;
-            bool fresh = false;
-            if (kind < 8u) {  // record item: {key, tag, orig, cpu, mem, gpu, avail, mask, ...}
-                const uint4* ip = reinterpret_cast<const uint4*>(&R->it[kind]);
-                const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2];
-                fresh = rfl((int32_t)i0.z) < 0;
-                a = make_uint4(i1.x, i1.y, i1.z, i1.w);       // cpu, mem, gpu, avail
-                b = make_uint4(i2.x, i0.x, i0.w, (uint32_t)t);  // mask, pos, orig, version
-            } else {  // dirty row of a ring winner
-                const uint4* rp = reinterpret_cast<const uint4*>(&S->rows[slot]);
-                a = rp[0];
-                const uint4 r1 = rp[1];
-                b = make_uint4(r1.x, r1.y, r1.z, (uint32_t)t);
-            }
-            a.x = (uint32_t)((int32_t)a.x - (int32_t)hd.x);
-            a.y = (uint32_t)((int32_t)a.y - (int32_t)hd.y);
-            a.z = (uint32_t)((int32_t)a.z - (int32_t)hd.z);
-            node = rfl((int32_t)b.z);
-            if (lane == 0) {
-                uint4* rp = reinterpret_cast<uint4*>(&S->rows[slot]);
-                rp[0] = a;
-                rp[1] = b;
-                if (fresh) {
-                    const uint32_t rel = (uint32_t)rfl((int32_t)b.y) - nb;
-                    __hip_atomic_fetch_or(&S->bitmap[rel >> 5], 1u << (rel & 31),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            if (fresh) nu = slot + 1;
-            ++placed;
-        }
-        oq = writelane(rfl((int32_t)hq.w), t & 63, oq);
-        ov = writelane(node, t & 63, ov);
-        if ((t & 63) == 63) {  // uniform: flush 64 placements
-            if (oq >= 0) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;
-            oq = -1;
-        }
-        cbar();
-        if (lane == 0)  // {decided, nu} in one 8-byte LDS store, after the row and bitmap
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(&S->decided),
-                               ((uint64_t)(uint32_t)nu << 32) | (uint32_t)(t + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (oq >= 0 && lane < (t & 63)) ((GAS int32_t*)out)[(int64_t)oq * kmax] = ov;  // last group
-    if (stop) lds_st(&S->halt, 1u);
-    MW_CLK(r1);
-    MW_ADD(17, r1 - r0);
-    MW_ADD(18, a_rw);
-    MW_ADD(19, t);
-    return CommitResult{t, stop, nu, placed};
+    return CommitResult{t, D.stop, D.nu, D.placed};
 }
 
 // All MW_WAVES waves of the block call this; returns the same result in every wave.
@@ -869,27 +934,22 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
     if (threadIdx.x < MW_R) S->rec[threadIdx.x].h.ready = 0u;
-    if (threadIdx.x < MW_DQ) S->dq[threadIdx.x].x = 0u;
     if (threadIdx.x == 0) {
-        S->decided = 0u;
+        S->dn = 0ull;
         S->halt = 0u;
-        S->nu = 0u;
         S->fail = 0u;
     }
     __syncthreads();
-    if (wave == 0 || (MW_RECORDER && wave == 1)) {
-        const CommitResult r = wave == 0 ? mw_decider(P, S, out, kmax)
-                                         : mw_recorder(P, S, out, kmax);
-        if (threadIdx.x == 64 * MW_RECORDER) {  // the recorder's result when it runs
+    if (wave == 0) {
+        const CommitResult r = mw_decider(P, S, out, kmax);
+        if (threadIdx.x == 0) {
             S->res[0] = r.done;
             S->res[1] = r.stop;
             S->res[2] = r.dirty;
             S->res[3] = r.placed;
         }
-    } else if (MW_RECORDER) {
-        mw_helper(P, S, rec, cand, bnd, wjob, wave - 1, T);  // waves 2.. : helpers 1..MW_H
-    } else if (MW_H == MW_WAVES - 1) {
-        mw_helper(P, S, rec, cand, bnd, wjob, wave, T);
+    } else if (!MW_IDLE4) {
+        mw_helper(P, S, rec, cand, bnd, wjob, wave, T);  // waves 1.. : helpers 1..MW_H
     } else if (wave != 4) {
         mw_helper(P, S, rec, cand, bnd, wjob, wave < 4 ? wave : wave - 1, T);
     }

@@ -111,13 +111,12 @@ def test_partition_free(name):
 def test_failed_load_leaves_no_node_table():
     nodes, jobs, parts = synth.make_config("c2", 512, 4096)
     big = (1 << 20) + 1  # one partition component above MAX_COMPONENT_NODES: FIT_E_INVAL late in the load
-    col = np.ones(big, np.int32)
+    col, mask = np.ones(big, np.int32), np.ones(big, np.uint32)  # kept alive across the call
     with Engine() as e:
         e.load_nodes(nodes)
         e.load_partitions(parts)
-        rc = _lib.lib().fit_load_nodes(e._h, big, *(fitgpu._ptr(col) for _ in range(4)),
-                                       fitgpu._ptr(np.ones(big, np.uint32)))
-        assert rc == _lib.FIT_E_INVAL
+        rc = _lib.lib().fit_load_nodes(e._h, big, *(fitgpu._ptr(col) for _ in range(4)), fitgpu._ptr(mask))
+        assert rc == _lib.FIT_E_INVAL, _lib.lib().fit_last_error()
         with pytest.raises(FitError) as ei:
             e.place(jobs)
         assert ei.value.code == _lib.FIT_E_STATE

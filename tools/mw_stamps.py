@@ -21,11 +21,7 @@ with Engine() as e:
 print({k: st[k] for k in ("ms_total", "ms_commit", "ms_device", "rounds")})
 tot = [sum(buf[c * W + i] for c in range(64)) for i in range(W)]
 dj, hj = max(tot[2], 1), max(tot[5], 1)
-print(f"decider: {tot[0] / dj:.0f} cyc/job, waiting for records {tot[1] / dj:.0f}, check+reduce {tot[7] / dj:.0f}, "
-      f"decide+publish {tot[8] / dj:.0f} cyc/job")
-print(f"decider: records not ready at the first read {tot[16] / dj:.3f} per job; "
-      f"recorder: {tot[17] / max(tot[19], 1):.0f} cyc/job, waiting for decisions {tot[18] / max(tot[19], 1):.0f}")
-print(f"decider waits in the first {8} jobs of each round: {tot[9] / dj:.0f} cyc/job (of the total wait)")
+print(f"decider: {tot[0] / dj:.0f} cyc/job, waiting for records (slow path) {tot[1] / dj:.0f} cyc/job")
 t0n = max(sum(buf[c * W + 11] for c in range(64)), 1)
 print(f"round's first tile: pickup delay {sum(buf[c * W + 10] for c in range(64)) / t0n / 100:.1f} us, "
       f"scan {sum(buf[c * W + 12] for c in range(64)) / t0n / 100:.1f} us (per task, {t0n} tasks)")

@@ -64,6 +64,38 @@ __global__ void k_ubench(unsigned long long* out, int* sink) {
     TIME(12, asm volatile(REP64("s_and_saveexec_b64 s[20:21], -1\ns_or_b64 exec, exec, s[20:21]\n") ::: "s20", "s21");)
     // 13: v_readfirstlane chain into s_cmp
     TIME(13, asm volatile(REP64("v_readfirstlane_b32 %1, %0\ns_cmp_eq_u32 %1, 0\n") : "+v"(v), "+s"(s) :: "scc");)
+    // 14: ballot → s_ff1 → v_readlane by that lane → v_add (select-a-lane round trip)
+    {
+        int x = lane;
+        TIME(14, asm volatile(REP64("v_cmp_eq_u32 vcc, 5, %0\ns_ff1_i32_b64 %1, vcc\nv_readlane_b32 %1, %0, %1\nv_add_u32 %0, %1, %0\n") : "+v"(x), "+s"(s) :: "vcc");)
+        r += x;
+    }
+    // 15: DPP row_ror:1 mov chain (2 wait states each)
+    TIME(15, asm volatile(REP64("s_nop 1\nv_mov_b32_dpp %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf\n") : "+v"(v));)
+    // 16: ds_bpermute dependent chain
+    {
+        int x = lane * 4;
+        TIME(16, asm volatile(REP64("ds_bpermute_b32 %0, %0, %0\ns_waitcnt lgkmcnt(0)\n") : "+v"(x));)
+        r += x;
+    }
+    // 17: ds_read_b128 dependent chain (address from the first dword)
+    {
+        int x = 0;
+        TIME(17, asm volatile(REP64("ds_read_b128 v[40:43], %0\ns_waitcnt lgkmcnt(0)\nv_and_b32 %0, 0, v40\n") : "+v"(x) :: "v40", "v41", "v42", "v43");)
+        r += x;
+    }
+    // 18: v_readlane (lane 0) → v_writelane m0 → (chain through the VGPR)
+    TIME(18, asm volatile("s_mov_b32 m0, 3\n" REP64("v_readlane_b32 %1, %0, 0\nv_writelane_b32 %0, %1, m0\n") : "+v"(v), "+s"(s) :: "m0");)
+    // 19: 8-lane 64-bit min step via DPP (2 movs + cmp + 2 cndmask) dependent chain
+    TIME(19, asm volatile("v_mov_b32 v40, %0\nv_mov_b32 v41, 0\n" REP64("s_nop 1\nv_mov_b32_dpp v42, v40 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\nv_mov_b32_dpp v43, v41 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\nv_cmp_lt_u64 vcc, v[42:43], v[40:41]\nv_cndmask_b32 v40, v40, v42, vcc\nv_cndmask_b32 v41, v41, v43, vcc\n") "v_add_u32 %0, %0, v40\n" : "+v"(v) :: "vcc", "v40", "v41", "v42", "v43");)
+    // 20: readfirstlane → s_cmp → s_cbranch_scc taken (loop control from a VGPR)
+    TIME(20, asm volatile(REP64("v_readfirstlane_b32 %1, %0\ns_cmp_eq_u32 %1, %1\ns_cbranch_scc1 1f\n1:\n") : "+v"(v), "+s"(s) :: "scc");)
+    // 21: v_cmp → s_and_b64 vcc, exec → s_cbranch_vccz (taken)
+    TIME(21, asm volatile(REP64("v_cmp_eq_u32 vcc, %0, %0\ns_and_b64 vcc, exec, vcc\ns_cbranch_vccz 1f\n1:\n") : "+v"(v) :: "vcc");)
+    // 22: v_add_u32 + v_cndmask dependent (VALU-only select chain)
+    TIME(22, asm volatile(REP64("v_cmp_gt_u32 vcc, %0, 7\nv_cndmask_b32 %0, 3, %0, vcc\n") : "+v"(v) :: "vcc");)
+    // 23: v_min3_u32 dep chain
+    TIME(23, asm volatile(REP64("v_min3_u32 %0, %0, %0, 60\n") : "+v"(v));)
     sink[lane] = v + r + s;
 }
 
@@ -82,7 +114,11 @@ int main() {
     const char* names[] = {"v_add dep", "s_add dep", "v_add 4 indep chains (per instr)", "readlane+s_add+v_add (per triple, +s_nop4)",
                            "ds_read dep+wait", "s_nop1+v_min_dpp", "v_cmp+cbranch(not taken) pair", "s_cmp+cbranch(taken) pair",
                            "s_waitcnt alone", "v_writelane m0", "ds_write+ds_read+wait", "v_cmp_u64+cndmask pair",
-                           "saveexec+restore pair", "readfirstlane+s_cmp pair"};
-    for (int i = 0; i < 14; ++i) printf("%-44s %6.2f cyc\n", names[i], h[i] / (64.0 * 16));
+                           "saveexec+restore pair", "readfirstlane+s_cmp pair",
+                           "ballot+s_ff1+readlane(sel)+v_add", "s_nop1+dpp row_ror mov", "ds_bpermute dep+wait",
+                           "ds_read_b128 dep+wait+v_and", "readlane+writelane(m0) pair", "8-lane u64 min step (5 VALU)",
+                           "readfirstlane+s_cmp+cbranch taken", "v_cmp+s_and vcc+cbranch_vccz", "v_cmp+cndmask pair",
+                           "v_min3 dep"};
+    for (int i = 0; i < 24; ++i) printf("%-44s %6.2f cyc\n", names[i], h[i] / (64.0 * 16));
     return 0;
 }
