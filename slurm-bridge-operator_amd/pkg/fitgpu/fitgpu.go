@@ -12,6 +12,7 @@ package fitgpu
 import "C"
 
 import (
+	"errors"
 	"fmt"
 	"runtime"
 	"unsafe"
@@ -20,6 +21,7 @@ import (
 const (
 	Unplaced = -1 // FIT_UNPLACED
 	Rejected = -2 // FIT_REJECTED
+	MaxK     = 8  // FIT_MAX_K: nodes per job (--nodes) fit_place supports
 )
 
 // Error carries a negative FIT_E_* code and the library's detail message.
@@ -67,8 +69,24 @@ type Nodes struct {
 	PartMask                              []uint32
 }
 
+// errLen is returned when the columns of one table differ in length: the library reads every
+// column for the same count, so a short slice would be read past its end.
+var errLen = errors.New("fitgpu: column slices of different lengths")
+
+func sameLen(n int, cols ...int) bool {
+	for _, c := range cols {
+		if c != n {
+			return false
+		}
+	}
+	return true
+}
+
 func (e *Engine) LoadNodes(n Nodes) error {
 	cnt := len(n.CPUFree)
+	if !sameLen(cnt, len(n.MemFreeMiB), len(n.GPUFree), len(n.AvailMin), len(n.PartMask)) {
+		return errLen
+	}
 	if cnt == 0 {
 		return check(C.fit_load_nodes(e.ctx, 0, nil, nil, nil, nil, nil))
 	}
@@ -82,6 +100,9 @@ func (e *Engine) LoadNodes(n Nodes) error {
 // LoadPartitions takes parseResources' limits (pkg/slurm-agent/parse.go:111-190), -1 = UNLIMITED.
 func (e *Engine) LoadPartitions(maxTimeMin, maxCPUs, maxMemMiB []int32) error {
 	p := len(maxTimeMin)
+	if !sameLen(p, len(maxCPUs), len(maxMemMiB)) {
+		return errLen
+	}
 	if p == 0 {
 		return check(C.fit_load_partitions(e.ctx, 0, nil, nil, nil))
 	}
@@ -98,18 +119,29 @@ type Jobs struct {
 type Stats = C.fit_stats
 
 // Place returns node ids (or Unplaced / Rejected) per job, kmax entries per job.
+// NodesK may be empty (every job takes one node); otherwise it has one entry per job.
 func (e *Engine) Place(j Jobs, kmax int) ([]int32, Stats, error) {
 	cnt := len(j.CPU)
-	out := make([]int32, cnt*kmax)
 	var st C.fit_stats
+	if kmax < 1 || kmax > MaxK {
+		return nil, st, fmt.Errorf("fitgpu: kmax %d outside [1, %d]", kmax, MaxK)
+	}
+	if !sameLen(cnt, len(j.MemMiB), len(j.GPU), len(j.WallMin), len(j.Part)) ||
+		(len(j.NodesK) != 0 && len(j.NodesK) != cnt) {
+		return nil, st, errLen
+	}
+	out := make([]int32, cnt*kmax)
 	if cnt == 0 {
 		return out, st, nil
+	}
+	var nk *C.uint16_t // NULL: every job takes one node
+	if len(j.NodesK) > 0 {
+		nk = (*C.uint16_t)(unsafe.Pointer(&j.NodesK[0]))
 	}
 	rc := C.fit_place(e.ctx, C.int32_t(cnt), (*C.int32_t)(unsafe.Pointer(&j.CPU[0])),
 		(*C.int32_t)(unsafe.Pointer(&j.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&j.GPU[0])),
 		(*C.int32_t)(unsafe.Pointer(&j.WallMin[0])), (*C.uint16_t)(unsafe.Pointer(&j.Part[0])),
-		(*C.uint16_t)(unsafe.Pointer(&j.NodesK[0])), C.int32_t(kmax),
-		(*C.int32_t)(unsafe.Pointer(&out[0])), &st)
+		nk, C.int32_t(kmax), (*C.int32_t)(unsafe.Pointer(&out[0])), &st)
 	return out, st, check(rc)
 }
 
@@ -130,6 +162,12 @@ type Releases struct {
 // LoadTimeline builds the backfill horizon (slots of slotMin minutes, <= 1024 slots) on top of
 // the node table of the last LoadNodes.
 func (e *Engine) LoadTimeline(slots, slotMin int, r Releases) error {
+	if !sameLen(len(r.Slot), len(r.CPU), len(r.MemMiB), len(r.GPU)) {
+		return errLen
+	}
+	if len(r.Off) > 0 && int(r.Off[len(r.Off)-1]) > len(r.Slot) {
+		return fmt.Errorf("fitgpu: Off ends at %d but there are %d release events", r.Off[len(r.Off)-1], len(r.Slot))
+	}
 	if len(r.Off) == 0 {
 		return check(C.fit_load_timeline(e.ctx, C.int32_t(slots), C.int32_t(slotMin), nil, nil, nil, nil, nil))
 	}
@@ -146,6 +184,9 @@ func (e *Engine) LoadTimeline(slots, slotMin int, r Releases) error {
 // node is Unplaced when nothing fits inside the horizon, Rejected for partition limits.
 func (e *Engine) PlaceBackfill(j Jobs) (node, start []int32, st Stats, err error) {
 	cnt := len(j.CPU)
+	if !sameLen(cnt, len(j.MemMiB), len(j.GPU), len(j.WallMin), len(j.Part)) {
+		return nil, nil, st, errLen
+	}
 	node, start = make([]int32, cnt), make([]int32, cnt)
 	if cnt == 0 {
 		return node, start, st, nil
