@@ -8,10 +8,14 @@ would hand them over), wall time of fit_load_nodes + fit_place end to end (H2D, 
 D2H of the placements).  That rate is `value`.  The same placement from HBM-resident inputs
 (fit_load_nodes_device + fit_place_device) is reported as `kernel_path_value`.
 
-N > 1 (default --scaling strong, --shard-mode nodes; SURVEY §8 e): ONE 100k × 1M placement split
-over the ranks by nodes, RCCL allgather of the candidate lists + u64 min-allreduce of the bounds
-per round.  --scaling weak gives every rank its own 100k × 1M cluster shard instead (no
-data-path collective; aggregate rate).
+N > 1 (default --scaling strong; SURVEY §8 e): ONE 100k × 1M placement split over the ranks.
+--shard-mode auto (default) gives each rank whole partition components (C3: 16 components, so
+2 per rank at N = 8) run by the persistent engine, then one RCCL merge; --shard-mode nodes splits
+every component's nodes (north_star's layout: RCCL allgather of the candidate lists + u64
+min-allreduce of the bounds per round, host-driven rounds).  Either way the step is bounded by
+the longest component's serial commit chain, so strong scaling is flat at best.
+--scaling weak gives every rank its own 100k × 1M cluster shard instead (no data-path
+collective; aggregate rate).
 
     python bench.py [--gpus N --steps K --warmup W] [--workload c3|c3o|c2|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -102,8 +106,9 @@ def parse_args():
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N>1: strong = one 100k x 1M placement split over the ranks (--shard-mode); "
                          "weak = every rank places its own 100k x 1M cluster shard (no data-path collective)")
-    ap.add_argument("--shard-mode", default="nodes", choices=["auto", "nodes", "components"],
-                    help="strong scaling split (north_star: nodes)")
+    ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
+                    help="strong scaling split: auto = partition components when there are >= N "
+                         "of them (C3), else nodes (north_star's node sharding)")
     return ap.parse_args()
 
 
@@ -309,8 +314,11 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
     ncomp = _components(nodes.part_mask)
     per_comp = nodes.n / max(ncomp, 1)
     par = min(threads, ncomp)
-    budget = 2e8 if tline is not None else 2e9
-    m_naive, m_comp, m_mc = budget / nodes.n, 3 * budget / per_comp, 3 * budget * par / per_comp
+    if tline is not None:  # a timeline evaluation walks runs of slots: ~20x a plain fit eval
+        m_naive, m_comp = 1e8 / nodes.n, 1.5e7 / per_comp
+    else:
+        m_naive, m_comp = 2e9 / nodes.n, 6e9 / per_comp
+    m_mc = m_comp * par
     if tline is not None:
         runs = [("naive-port", 1, m_naive, lambda s: po.ref_place_tl(nodes, tline, s, parts)[2],
                  "oracle/fitref_tl.c ref_place_tl (SPEC §2b, dense timelines, every node per job)"),

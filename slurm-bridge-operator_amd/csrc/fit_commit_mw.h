@@ -309,11 +309,18 @@ __device__ __forceinline__ uint32_t wave_min32_l63(uint32_t v) {
     return dpp_min32<0x143, 0xc>(v);
 }
 // 64-bit minimum over the wave (uniform): two 32-bit passes
+// (the second pass only when several lanes hold the minimum high word: a uniform branch)
 __device__ __forceinline__ uint64_t wave_min64_2pass(uint64_t v) {
     const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
     const uint32_t mh = (uint32_t)__builtin_amdgcn_readlane((int)wave_min32_l63(hi), 63);
-    const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane(
-        (int)wave_min32_l63(hi == mh ? lo : 0xffffffffu), 63);
+    const uint64_t eq = __ballot(hi == mh);
+    uint32_t ml;
+#ifndef MW_NO_TIESKIP
+    if (__popcll(eq) == 1)
+        ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(eq));
+    else
+#endif
+        ml = (uint32_t)__builtin_amdgcn_readlane((int)wave_min32_l63(hi == mh ? lo : 0xffffffffu), 63);
     return ((uint64_t)mh << 32) | ml;
 }
 // minimum over the wave, valid in lane 63
