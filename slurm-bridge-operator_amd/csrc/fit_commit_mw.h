@@ -725,19 +725,19 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
         const uint64_t rk0 = mw_key(R.a.x, R.a.y, R.a.z, R.a.w, (uint32_t)R.b.x, (uint32_t)R.b.y,
                                     jc, jm, jg, jw, jp);
         const uint64_t rkey = live ? rk0 : KEY_INF;
+        const uint32_t ip = x.i0.x;
         // item staleness: its node is in the live ring.  Lanes 8..15 take a copy of the ring
         // (row_ror:8), so row_ror:k, k = 0..7, shows lane i < 8 every ring entry once.
         const uint32_t P0 = live ? (uint32_t)R.b.y : 0xffffffffu;  // positions are < 2^29
         const uint32_t P8 = dpp32<0x128>(P0);
         const uint32_t P2 = (lane & 8) ? P8 : P0;
-        const uint32_t ip = x.i0.x;
         const uint32_t d0 = ip ^ P2, d1 = dpp_ror_xor<1, true>(P2, ip),
                        d2 = dpp_ror_xor<2, false>(P2, ip), d3 = dpp_ror_xor<3, false>(P2, ip),
                        d4 = dpp_ror_xor<4, false>(P2, ip), d5 = dpp_ror_xor<5, false>(P2, ip),
                        d6 = dpp_ror_xor<6, false>(P2, ip), d7 = dpp_ror_xor<7, false>(P2, ip);
-        const uint32_t dmin = min(min(min(d0, d1), min(d2, d3)), min(min(d4, d5), min(d6, d7)));
+        const bool stale = min(min(min(d0, d1), min(d2, d3)), min(min(d4, d5), min(d6, d7))) == 0u;
         const uint64_t ik0 = ((uint64_t)x.i0.y << 32) | ip;
-        const uint64_t ikey = (lane < n && dmin != 0u) ? ik0 : KEY_INF;
+        const uint64_t ikey = (lane < n && !stale) ? ik0 : KEY_INF;
         const bool tr = rkey < ikey;  // this lane's ring row beats its item
         const uint64_t cand = tr ? rkey : ikey;
         // the winner's fields, demand already subtracted (selected per lane, read from one)
