@@ -416,6 +416,17 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     if (nc == 0) return 0;
     const int64_t wcap = std::min(c->wmax, 8192);  // k_engine's per-tile counters: 128 job tiles
     const int64_t per_comp_cand = wcap * MAX_SLICES * KS;
+    // keys per block-slice: KS, halved (slices doubled, the same MAX_SLICES * KS candidates per
+    // job) while a wave's sub-slice would exceed sub_target nodes — a round's first job tile, which
+    // the commit waits for, then spreads over more blocks.  C3o (one 100k-node component): KS 16
+    // 552 ms, 8 471 ms, 4 441 ms, 2 480 ms (the bound B, a minimum over more slices of fewer keys,
+    // turns tight: 891 rescans); C3 / C2 components stay at KS (sub-slices of 98 / 64 nodes).
+    int sub_target = 256, ks_min = 4;
+    if (const char* e = getenv("FIT_SUB_TARGET")) sub_target = std::max(MIN_SUB, atoi(e));
+    if (const char* e = getenv("FIT_KS_MIN")) ks_min = std::max(2, std::min(KS, atoi(e)));
+    // a multi-node job needs k keys <= B on one slice: the slice that sets B has ks of them, all
+    // clean when the job opens a round, so ks >= kmax keeps every round's first job resolvable
+    while (ks_min < kmax) ks_min *= 2;
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
         c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
         c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
@@ -428,8 +439,12 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.nb = s.sb = c->nb[k];
         s.ne = s.se = c->nb[k + 1];
         const int32_t len = s.ne - s.nb;
-        s.sub = std::max(MIN_SUB, (len + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
-        s.nslice = std::max(1, (len + SCAN_WAVES * s.sub - 1) / (SCAN_WAVES * s.sub));
+        for (s.ks = KS;; s.ks /= 2) {
+            const int slices = MAX_SLICES * KS / s.ks;
+            s.sub = std::max(MIN_SUB, (len + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
+            s.nslice = std::max(1, (len + SCAN_WAVES * s.sub - 1) / (SCAN_WAVES * s.sub));
+            if (s.sub <= sub_target || s.ks / 2 < ks_min) break;
+        }
         s.jstart = jb[k];
         s.jend = jb[k + 1];
         s.cand_off = (int64_t)i * per_comp_cand;
@@ -596,6 +611,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
             P.sb = std::min(P.ne, P.nb + per * srank);
             P.se = std::min(P.ne, P.sb + per);
             // sub-slices of >= MIN_SUB nodes, at most MAX_SLICES block-slices per job per rank
+            P.ks = KS;
             P.sub = std::max(MIN_SUB, (per + SCAN_WAVES * MAX_SLICES - 1) / (SCAN_WAVES * MAX_SLICES));
             P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
             epl = std::max(epl, (shards * P.nslice * KS + 63) / 64);
@@ -728,6 +744,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         s.nb = s.sb = c->nb[k];
         s.ne = s.se = c->nb[k + 1];
         const int32_t len = s.ne - s.nb;
+        s.ks = TL_KS;
         s.sub = std::max(tl_min_sub, (len + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
         s.nslice = std::max(1, (len + SCAN_WAVES * s.sub - 1) / (SCAN_WAVES * s.sub));
         s.jstart = jb[k];
@@ -853,6 +870,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
             P.se = std::min(P.ne, P.sb + per);
             // more, shorter block-slices than the plain fit: a run walk costs more per node, so
             // the scan wants more waves in flight; candidate entries per job stay <= 256
+            P.ks = TL_KS;
             P.sub = std::max(tl_min_sub, (per + SCAN_WAVES * slices - 1) / (SCAN_WAVES * slices));
             P.nslice = std::max(1, (per + SCAN_WAVES * P.sub - 1) / (SCAN_WAVES * P.sub));
             epl = std::max(epl, (shards * P.nslice * TL_KS + 63) / 64);

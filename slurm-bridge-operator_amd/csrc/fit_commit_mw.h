@@ -218,6 +218,7 @@ __device__ __forceinline__ CompPlan plan_sgpr(const CompPlan& q) {
     p.jbase = rfl(q.jbase);
     p.w = rfl(q.w);
     p.blk0 = rfl(q.blk0);
+    p.ks = rfl(q.ks);
     p.cand_off = (int64_t)(((uint64_t)(uint32_t)rfl((int32_t)(q.cand_off >> 32)) << 32) |
                            (uint32_t)rfl((int32_t)q.cand_off));
     p.slot0 = rfl(q.slot0);
@@ -563,7 +564,7 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     const CompPlan P = plan_sgpr(Pref);
     MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
-    const int E = P.nslice * KS;
+    const int E = P.nslice * P.ks;
     bool has[MW_EPL];       // candidate entry lane + 64 e of the job's E entries
     int64_t eoff[MW_EPL];
 #pragma unroll

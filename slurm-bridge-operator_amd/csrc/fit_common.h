@@ -68,12 +68,29 @@ __device__ __forceinline__ uint64_t wave_min_key_lane(uint64_t v, int& lane) {
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
 
-// sorted ascending insert of x into key[0..K) dropping the largest (static indices only)
+// sorted ascending insert of x (< KEY_INF) into key[0..K) dropping the largest (static indices
+// only).  Entry i becomes key[i-1] if x < key[i-1], x if key[i-1] <= x < key[i], else key[i]:
+// with the K compares c[i] = x < key[i] issued first (independent, so no compare → select
+// hazard stalls), the high word is the clamp max(hi[i-1], min(hi[i], x.hi)) — exact because the
+// list is sorted; one v_med3_u32 — and only the low word needs the two selects: 4 VALU per entry
+// instead of two 64-bit min/max (2 compares + 4 selects + 2 hazard nops through one SGPR pair).
 template <int K>
 __device__ __forceinline__ void topk_insert(uint64_t (&key)[K], uint64_t x) {
+    const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
+    bool c[K];
 #pragma unroll
-    for (int i = K - 1; i > 0; --i) key[i] = umax64(key[i - 1], umin64(key[i], x));
-    key[0] = umin64(key[0], x);
+    for (int i = 0; i < K; ++i) c[i] = x < key[i];
+    uint64_t n[K];
+    n[0] = c[0] ? x : key[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        const uint32_t a = (uint32_t)(key[i - 1] >> 32), b = (uint32_t)(key[i] >> 32);
+        const uint32_t h = max(min(a, b), min(max(a, b), xh));  // med3 (= the clamp: a <= b)
+        const uint32_t l = c[i - 1] ? (uint32_t)key[i - 1] : (c[i] ? xl : (uint32_t)key[i]);
+        n[i] = ((uint64_t)h << 32) | l;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) key[i] = n[i];
 }
 
 // (list, bound) pairs: every node of the covered range that is not in the sorted list has a
@@ -114,8 +131,9 @@ __device__ __forceinline__ int find_comp(const CompPlan* __restrict__ plan, int 
 // One (job-lane, node-row) evaluation.  Node fields are clamped to >= -1 when the table is built
 // (k_gather_nodes) and demands are >= 0, so every difference below is exact in int32; the pair
 // is feasible iff no difference is negative and the partition bit is set.
+template <int K>
 __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& J,
-                                         uint64_t (&key)[KS], uint32_t& lim) {
+                                         uint64_t (&key)[K], uint32_t& lim) {
     const int32_t dc = r.cpu - J.cpu, dm = r.mem - J.mem, dg = r.gpu - J.gpu;
     const int32_t da = r.avail - J.wall;
     const int32_t dp = (int32_t)((r.mask & J.pbit) - 1u);  // -1: not a member (or idle lane)
@@ -124,23 +142,25 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
                         min((uint32_t)dm >> 10, 4095u);
     if (bad >= 0 && sc <= lim) {
         topk_insert(key, ((uint64_t)sc << 32) | (uint32_t)x);
-        const uint64_t last = key[KS - 1];
+        const uint64_t last = key[K - 1];
         lim = last == KEY_INF ? 0xffffffffu : (uint32_t)(last >> 32) - 1u;
     }
 }
 
 // -------------------------------------------------------------------------------- k_scan
 // Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices (one per wave).
-// Each wave keeps the exact top-KS of its sub-slice; the 8 lists are merged through LDS in a
-// bitonic tree, giving the exact top-KS (and bound) of the block-slice.
-template <bool PERSISTENT>
+// Each wave keeps the exact top-K of its sub-slice; the 8 lists are merged through LDS in a
+// bitonic tree, giving the exact top-K (and bound) of the block-slice.  K = P.ks (KS, or fewer
+// keys over more block-slices for a large component: the same candidates per job, but a round's
+// first job tile — which the commit waits for — is spread over more blocks).
+template <bool PERSISTENT, int K>
 __device__ __forceinline__ void scan_tile(
     const CompPlan& P, int tile, int s, const NodeRec* __restrict__ rec,
     const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
     const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
     const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
     const uint16_t* __restrict__ jk, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
-    JobRec* __restrict__ wjob, uint64_t (*xk)[KS][64]) {
+    JobRec* __restrict__ wjob, uint64_t (*xk)[K][64]) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -157,9 +177,9 @@ __device__ __forceinline__ void scan_tile(
     J.k = active ? (jk ? max((int)jk[J.q], 1) : 1) : 1;
     J.pad = 0;
 
-    uint64_t key[KS];
+    uint64_t key[K];
 #pragma unroll
-    for (int i = 0; i < KS; ++i) key[i] = KEY_INF;
+    for (int i = 0; i < K; ++i) key[i] = KEY_INF;
     // candidate test: score <= lim, lim = (K-th score - 1) once the list is full.  An equal
     // score never beats the K-th entry (positions only grow); a spurious insert when the K-th
     // score is 0 is dropped by the 64-bit insertion network, so the list stays exact.
@@ -181,29 +201,29 @@ __device__ __forceinline__ void scan_tile(
     for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
         if (wave >= h && wave < 2 * h) {
 #pragma unroll
-            for (int i = 0; i < KS; ++i) xk[wave - h][i][lane] = key[i];
+            for (int i = 0; i < K; ++i) xk[wave - h][i][lane] = key[i];
         }
         __syncthreads();
         if (wave < h) {
-            uint64_t o[KS];
+            uint64_t o[K];
 #pragma unroll
-            for (int i = 0; i < KS; ++i) o[i] = xk[wave][i][lane];
+            for (int i = 0; i < K; ++i) o[i] = xk[wave][i][lane];
             merge_lists(key, o);
         }
         __syncthreads();
     }
     if (wave != 0 || !active) return;  // (no barrier follows inside scan_tile)
-    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KS;
+    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * K;
 #pragma unroll
-    for (int i = 0; i < KS; i += 2) {
+    for (int i = 0; i < K; i += 2) {
         ulonglong2 v;
         v.x = key[i];
         v.y = key[i + 1];
         *reinterpret_cast<ulonglong2*>(dst + i) = v;
     }
-    if (key[KS - 1] != KEY_INF)
+    if (key[K - 1] != KEY_INF)
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
-                  (unsigned long long)key[KS - 1]);
+                  (unsigned long long)key[K - 1]);
     if (s == 0) wjob[P.slot0 + t] = J;
 }
 
@@ -478,7 +498,7 @@ __device__ __forceinline__ CommitResult commit_window(
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (single wave: LDS in order)
 
-    const int per_rank = P.nslice * KS;
+    const int per_rank = P.nslice * P.ks;
     const int E = nranks * per_rank;
     int64_t off[EPL];
     bool has[EPL];

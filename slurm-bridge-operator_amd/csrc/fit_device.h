@@ -56,6 +56,7 @@ struct alignas(16) CompPlan {
     int32_t jbase;       // first window job's index into the component job list
     int32_t w;           // window size (jobs)
     int32_t blk0;        // first fit_scan block of this component
+    int32_t ks;          // keys kept per (job, block-slice): KS, or fewer for a large component
     int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
     int32_t slot0;       // first window slot (global over components)
 };
@@ -68,6 +69,7 @@ struct CompState {
     int64_t cand_off;      // fixed candidate region of this component
     int32_t slot0;         // fixed window slot region
     int32_t wmin, wmax;
+    int32_t ks;            // keys per (job, block-slice) (CompPlan::ks)
 };
 
 struct CompOut {

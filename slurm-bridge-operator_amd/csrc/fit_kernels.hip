@@ -27,7 +27,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan(
     // integer division expands to VALU code: pin the (uniform) results to SGPRs
     const int tile = __builtin_amdgcn_readfirstlane(local / P.nslice);
     const int s = __builtin_amdgcn_readfirstlane(local - tile * P.nslice);
-    scan_tile<false>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk);
+    scan_tile<false, KS>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk);
 }
 
 template <int EPL>

@@ -66,6 +66,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             P.se = S.se;
             P.nslice = S.nslice;
             P.sub = S.sub;
+            P.ks = S.ks;
             P.jbase = cursor;
             P.w = w;
             P.blk0 = 0;
@@ -140,6 +141,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
                 break;
             }
+            if (R.done == 0) {  // the next round would rescan the same state: never progresses
+                if (threadIdx.x == 0) atomicOr(&ctl->error, 4u);
+                break;
+            }
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
             tw += t1 - t0;
             tc += t2 - t1;
@@ -165,7 +170,6 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     }
 
     // ====================================================================== scan worker
-    uint64_t(*xk)[KS][64] = reinterpret_cast<uint64_t(*)[KS][64]>(smem);
     unsigned long long* task_slot =
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
     int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
@@ -213,8 +217,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
             const CompPlan P = plans[c];
-            scan_tile<true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,
-                            xk);
+            switch (P.ks) {  // block-uniform; the host picks one of these (engine.cpp)
+#define SCAN_K(K_)                                                                               \
+    case K_:                                                                                      \
+        scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd,   \
+                            wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem));                   \
+        break;
+                SCAN_K(16)
+                SCAN_K(8)
+                SCAN_K(4)
+                default:
+                SCAN_K(2)
+#undef SCAN_K
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
 #ifdef FIT_STAMPS
             if (threadIdx.x == 0 && tile == 0) {  // the round's first tile: pickup delay, scan time

@@ -59,6 +59,25 @@ def test_c3o_overlapping_partitions_prefix(engine, monkeypatch):
     assert st["components"] == 1
 
 
+@pytest.mark.parametrize("ks_min", ["8", "4", "2"])
+def test_fewer_keys_per_slice(ks_min, monkeypatch):
+    """A large component keeps fewer keys per block-slice over more slices (engine.cpp: KS 16 →
+    8 → 4 while a wave's sub-slice exceeds FIT_SUB_TARGET nodes); forced down to KS 8 / 4 / 2 on
+    one 20,000-node component for single-node jobs (decider / helper commit), and for C4's
+    multi-node jobs (single-wave commit), where the engine keeps KS >= kmax (8) so that every
+    round's first job stays resolvable."""
+    monkeypatch.setenv("FIT_SUB_TARGET", "64")
+    monkeypatch.setenv("FIT_KS_MIN", ks_min)
+    nodes, jobs, parts = synth.make_config("c3o", 20000, 50000)
+    check_parity(nodes, jobs, parts)
+    nodes, jobs, parts = synth.make_config("c4", 20000, 20000)
+    nodes.part_mask = nodes.part_mask | np.uint32(1 << 16)  # one component
+    jobs.part = np.where(np.arange(jobs.j) % 10 == 3, 16, jobs.part).astype(np.uint16)
+    parts = synth.gen_partitions(synth.SEEDS["c4"], 17)
+    st = check_parity(nodes, jobs, parts, kmax=8)
+    assert st["components"] == 1
+
+
 @pytest.mark.parametrize("wmin,wmax", [(1, 1), (1, 8), (64, 64), (512, 65536)])
 def test_window_policies_c2(wmin, wmax):
     nodes, jobs, parts = synth.make_config("c2", 512, 8192)
