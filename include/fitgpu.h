@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 3
+#define FITGPU_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -240,6 +240,45 @@ int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32
  * gpu2-ib), NUL-separated into buf; returns the count, FIT_E_PARSE or FIT_E_INVAL (buf too
  * small).  The fix for parsePartition's split of "Nodes=node[1-3,5]" (parse.go:278-289). */
 int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen);
+
+/* ---- batched admission (CreatePod's call site) -----------------
+ * The virtual kubelet calls CreatePod(ctx, *v1.Pod) (pkg/slurm-virtual-kubelet/provider.go:35-60)
+ * from 10 concurrent PodSyncWorkers (options/options.go:107), one pod per call; a non-nil error
+ * makes the library retry the pod later.  A fit_admitter coalesces those calls: fit_admit blocks
+ * while its request joins the open batch; the batch closes max_wait_us after its first request
+ * (or at max_batch requests), is ordered by (priority, arrival), placed with ONE fit_place, and
+ * every caller returns with its own result.  Placements consume the context's node table, so
+ * later batches see them until the next fit_admitter_load_nodes (the node ticker,
+ * provider.go:470-488).  All calls are thread-safe; while an admitter owns a context, use the
+ * context only through it.  fit_admitter_destroy fails still-queued requests with FIT_E_STATE. */
+typedef struct fit_admitter fit_admitter;
+typedef struct {
+    int64_t priority;  /* smaller first (e.g. pod creation time); ties keep arrival order   */
+    int32_t cpu;       /* per-node demand as fit_job_demand derives it                      */
+    int32_t mem_mib;
+    int32_t gpu;
+    int32_t wall_min;
+    uint16_t part;     /* partition index (fit_load_partitions order)                       */
+    uint16_t nodes_k;  /* --nodes, 0 = 1, <= FIT_MAX_K                                      */
+} fit_admit_req;
+typedef struct {
+    int32_t node[FIT_MAX_K]; /* node ids (nodes_k of them, rest -1), or node[0] = FIT_UNPLACED
+                                (no capacity now: retry) / FIT_REJECTED (partition limits)  */
+    int64_t batch;           /* batch sequence number (0, 1, ...)                           */
+    int32_t batch_jobs;      /* requests placed together in that batch                      */
+    int32_t order;           /* this request's index in the batch's placement order        */
+} fit_admit_res;
+int fit_admitter_create(fit_ctx* ctx, int32_t max_batch, int32_t max_wait_us, fit_admitter** out);
+/* Blocks until the request's batch is placed.  FIT_OK (result in *res), FIT_E_INVAL (bad
+ * request: negative demand, nodes_k > FIT_MAX_K; not queued), FIT_E_STATE (admitter shutting
+ * down / no node table), or the batch's fit_place error. */
+int fit_admit(fit_admitter* a, const fit_admit_req* req, fit_admit_res* res);
+int fit_admitter_load_nodes(fit_admitter* a, int32_t n, const int32_t* cpu_free,
+                            const int32_t* mem_free, const int32_t* gpu_free,
+                            const int32_t* avail_min, const uint32_t* part_mask);
+int fit_admitter_partition_free(fit_admitter* a, int32_t p, int64_t* cpu, int64_t* mem_mib,
+                                int64_t* gpu);
+void fit_admitter_destroy(fit_admitter* a);
 
 #ifdef __cplusplus
 }

@@ -1371,3 +1371,7 @@ int fit_read_timeline(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
 }
 
 }  // extern "C"
+
+namespace fitgpu {
+void set_last_error(const char* msg) { g_last_error = msg; }  // admit.cpp: the batch's error
+}  // namespace fitgpu

@@ -46,6 +46,10 @@ namespace fitgpu {
 #endif
 constexpr int MW_M = MW_ITEMS;          // items per pre-resolved record (> snapshot lag)
 constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once job t-8 is decided
+#ifndef MW_SNAP
+#define MW_SNAP MW_ITEMS  // a helper snapshots job t's state once the decider has resolved t - (MW_SNAP - 1)
+#endif
+static_assert(MW_SNAP >= 1 && MW_SNAP <= MW_ITEMS, "a later snapshot only shortens the ring span");
 constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
 #ifndef MW_IDLE4
 #define MW_IDLE4 0  // 1: wave 4 (the decider's SIMD partner) stays idle, six helpers
@@ -441,7 +445,7 @@ __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
         MW_CLK(hw0_);                                                                          \
         for (unsigned sp_ = 0;; ++sp_) {                                                       \
             dn_ = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
-            const int lag_ = t - (MW_M - 1) - rfl((int32_t)(uint32_t)dn_);                     \
+            const int lag_ = t - (MW_SNAP - 1) - rfl((int32_t)(uint32_t)dn_);                  \
             if (lag_ <= 0) break;                                                              \
             if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
             if (sp_ > MW_SPIN_LIMIT) {                                                         \
@@ -574,7 +578,7 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     }
     const int wlast = P.w - 1;
     const int z = opaque_zero();
-    int t = h - 1;
+    int t = rfl(h - 1);  // uniform (h arrives in a VGPR: the callee is out of line)
 
     uint64_t kk[3][MW_EPL], jbd[3];
     JobRec jr[3];

@@ -26,8 +26,8 @@ import numpy as np
 
 from ._lib import (FIT_E_PARSE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS,
                    FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32,
-                   FIT_XCHG_MIN_U64, XCHG_FN, FitError, FitJobResources, FitNode, FitOpts, FitResources,
-                   FitStats, check, lib)
+                   FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError, FitJobResources, FitNode,
+                   FitOpts, FitResources, FitStats, check, lib)
 
 __all__ = [
     "Engine", "FitError", "ErrDurationIsUnlimited", "ParseDuration", "parse_resources", "parse_nodes",
@@ -35,7 +35,7 @@ __all__ = [
     "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
     "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
     "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS", "expand_hostlist", "ingest_nodes",
-    "FIT_FLAG_COLLECTIVES",
+    "FIT_FLAG_COLLECTIVES", "Admitter",
 ]
 
 
@@ -382,3 +382,55 @@ class Engine:
         c, m, g = C.c_int64(), C.c_int64(), C.c_int64()
         check(lib().fit_partition_free(self._h, p, C.byref(c), C.byref(m), C.byref(g)), "fit_partition_free")
         return {"cpu": c.value, "mem_mib": m.value, "gpu": g.value}
+
+
+class Admitter:
+    """Batched admission over one Engine (include/fitgpu.h "batched admission"; the CreatePod
+    call site of pkg/slurm-virtual-kubelet/provider.go:35-60).  `admit` blocks the calling thread
+    until its batch is placed (ctypes releases the GIL, so threads admit concurrently, as the 10
+    PodSyncWorkers do) and returns (nodes, batch, batch_jobs, order); nodes[0] is FIT_UNPLACED /
+    FIT_REJECTED when the pod cannot be placed now."""
+
+    def __init__(self, engine: Engine, max_batch: int = 1024, max_wait_us: int = 2000):
+        self._engine = engine  # keeps the context alive
+        h = C.c_void_p()
+        check(lib().fit_admitter_create(engine._h, max_batch, max_wait_us, C.byref(h)), "fit_admitter_create")
+        self._h = h
+
+    def admit(self, priority: int, cpu: int, mem_mib: int, gpu: int = 0, wall_min: int = 0,
+              part: int = 0, nodes_k: int = 1):
+        q = FitAdmitReq(priority, cpu, mem_mib, gpu, wall_min, part, nodes_k)
+        r = FitAdmitRes()
+        check(lib().fit_admit(self._h, C.byref(q), C.byref(r)), "fit_admit")
+        k = max(nodes_k, 1)
+        nodes = [r.node[i] for i in range(k)] if r.node[0] >= 0 else [r.node[0]]
+        return nodes, r.batch, r.batch_jobs, r.order
+
+    def load_nodes(self, nodes):
+        cols = [np.ascontiguousarray(nodes.cpu_free, np.int32), np.ascontiguousarray(nodes.mem_free, np.int32),
+                np.ascontiguousarray(nodes.gpu_free, np.int32), np.ascontiguousarray(nodes.avail_min, np.int32),
+                np.ascontiguousarray(nodes.part_mask, np.uint32)]
+        check(lib().fit_admitter_load_nodes(self._h, len(cols[0]), *[_ptr(c) for c in cols]),
+              "fit_admitter_load_nodes")
+        self._engine.n = len(cols[0])
+
+    def partition_free(self, p: int):
+        c, m, g = C.c_int64(), C.c_int64(), C.c_int64()
+        check(lib().fit_admitter_partition_free(self._h, p, C.byref(c), C.byref(m), C.byref(g)),
+              "fit_admitter_partition_free")
+        return {"cpu": c.value, "mem_mib": m.value, "gpu": g.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fit_admitter_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+

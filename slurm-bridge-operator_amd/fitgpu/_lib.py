@@ -34,6 +34,8 @@ EXPORTS = [
     "fit_pod_request", "fit_job_demand", "fit_partition_capacity",
     "fit_load_timeline", "fit_load_timeline_device", "fit_place_tl", "fit_place_tl_device",
     "fit_read_timeline", "fit_ingest_nodes", "fit_expand_hostlist",
+    "fit_admitter_create", "fit_admit", "fit_admitter_load_nodes", "fit_admitter_partition_free",
+    "fit_admitter_destroy",
 ]
 
 
@@ -61,6 +63,20 @@ class FitStats(C.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+FIT_MAX_K = 8
+
+
+class FitAdmitReq(C.Structure):
+    _fields_ = [("priority", C.c_int64), ("cpu", C.c_int32), ("mem_mib", C.c_int32),
+                ("gpu", C.c_int32), ("wall_min", C.c_int32), ("part", C.c_uint16),
+                ("nodes_k", C.c_uint16)]
+
+
+class FitAdmitRes(C.Structure):
+    _fields_ = [("node", C.c_int32 * FIT_MAX_K), ("batch", C.c_int64), ("batch_jobs", C.c_int32),
+                ("order", C.c_int32)]
 
 
 class FitResources(C.Structure):
@@ -112,6 +128,13 @@ def lib() -> C.CDLL:
         L.fit_ingest_nodes.argtypes = [C.c_char_p, C.c_char_p, i32, i32, P, P, P, P, P, C.c_char_p, i32]
         L.fit_expand_hostlist.argtypes = [C.c_char_p, C.c_char_p, i32]
         L.fit_partition_free.argtypes = [P, i32, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
+        L.fit_admitter_create.argtypes = [P, i32, i32, C.POINTER(P)]
+        L.fit_admit.argtypes = [P, C.POINTER(FitAdmitReq), C.POINTER(FitAdmitRes)]
+        L.fit_admitter_load_nodes.argtypes = [P, i32, P, P, P, P, P]
+        L.fit_admitter_partition_free.argtypes = [P, i32, C.POINTER(i64), C.POINTER(i64),
+                                                  C.POINTER(i64)]
+        L.fit_admitter_destroy.argtypes = [P]
+        L.fit_admitter_destroy.restype = None
         L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]
         L.fit_parse_nodes.argtypes = [C.c_char_p, C.POINTER(FitNode), i32]

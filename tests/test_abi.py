@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.fit_abi_version() == 3
+    assert L.fit_abi_version() == 4
     assert L.fit_strerror(_lib.FIT_E_NODEV) == b"no usable gfx950 device"
 
 
@@ -54,3 +54,8 @@ def test_null_args_are_rejected():
     assert L.fit_load_nodes(None, 0, None, None, None, None, None) == _lib.FIT_E_INVAL
     assert L.fit_place(None, 0, None, None, None, None, None, None, 1, None, None) == _lib.FIT_E_INVAL
     del h
+    a = C.c_void_p()
+    assert L.fit_admitter_create(None, 16, 1000, C.byref(a)) == _lib.FIT_E_INVAL
+    assert L.fit_admit(None, None, None) == _lib.FIT_E_INVAL
+    assert L.fit_admitter_load_nodes(None, 0, None, None, None, None, None) == _lib.FIT_E_INVAL
+    L.fit_admitter_destroy(None)  # no-op
