@@ -15,7 +15,8 @@ every component's nodes (north_star's layout: RCCL allgather of the candidate li
 min-allreduce of the bounds per round, host-driven rounds).  Either way the step is bounded by
 the longest component's serial commit chain, so strong scaling is flat at best.
 --scaling weak gives every rank its own 100k × 1M cluster shard instead (no data-path
-collective; aggregate rate).
+collective; aggregate rate); a strong N > 1 run also reports that rate as the extra key
+`weak_scaling` (--no-weak-extra skips it).
 
     python bench.py [--gpus N --steps K --warmup W] [--workload c3|c3o|c2|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -106,6 +107,8 @@ def parse_args():
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N>1: strong = one 100k x 1M placement split over the ranks (--shard-mode); "
                          "weak = every rank places its own 100k x 1M cluster shard (no data-path collective)")
+    ap.add_argument("--no-weak-extra", action="store_true",
+                    help="N>1 strong: skip the extra weak-scaling leg (the `weak_scaling` key)")
     ap.add_argument("--shard-mode", default="auto", choices=["auto", "nodes", "components"],
                     help="strong scaling split: auto = partition components when there are >= N "
                          "of them (C3), else nodes (north_star's node sharding)")
@@ -128,18 +131,16 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fitgpu import (FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, Engine, nccl_unique_id,
-                        synth)
+    from fitgpu import (FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, Engine, TorchHostExchange,
+                        nccl_unique_id, synth)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world == 1 and a.gpus > 1:
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    if a.rehearse:
+    if a.rehearse:  # test only: all ranks on cuda:0, gloo; strong runs exchange through the host
         local = 0
-        if a.scaling != "weak":
-            raise SystemExit("--rehearse supports --scaling weak only")
     torch.cuda.set_device(local)
     weak = world > 1 and a.scaling == "weak"
     nid = None
@@ -148,7 +149,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        if not weak:
+        if not weak and not a.rehearse:
             obj = [nccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             nid = obj[0]
@@ -165,6 +166,8 @@ def main():
     mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
     if weak:
         eng = Engine(device=local)  # independent shard: no collective in the data path
+    elif a.rehearse:
+        eng = Engine(device=local, rank=rank, world=world, shard_mode=mode, exchange=TorchHostExchange())
     else:
         eng = Engine(device=local, rank=rank, world=world, nccl_id=nid, shard_mode=mode)
     eng.load_partitions(parts)
@@ -289,9 +292,45 @@ def main():
     }
     if cpu:
         line["speedup_vs_cpu"] = {v["kind"]: round(value / v["value"], 1) for v in cpu["variants"]}
+    if world > 1 and not weak and not a.no_weak_extra:
+        # extra key: the same ranks, each placing its own 100k x 1M cluster shard (disjoint generator
+        # slice, its own partitions; no collective in the data path), aggregate rate, host path
+        eng.close()
+        if tl:
+            wn, wt, wj, wp = synth.make_c5(shard=rank)
+        else:
+            wn, wj, wp = synth.make_config(a.workload, shard=rank)
+        weng = Engine(device=local)
+        weng.load_partitions(wp)
+        wkeep = []
+        wh_nodes = synth.Nodes(*(_pinned(wkeep, x) for x in (wn.cpu_free, wn.mem_free, wn.gpu_free,
+                                                              wn.avail_min, wn.part_mask)))
+        wh_jobs = synth.Jobs(*(_pinned(wkeep, x) for x in (wj.cpu, wj.mem, wj.gpu, wj.wall, wj.part,
+                                                            wj.nodes_k)))
+        wh_out = _pinned(wkeep, np.zeros(wj.j, np.int32))
+        if tl:
+            wh_tl = synth.Timeline(wt.slots, wt.slot_min,
+                                   *(_pinned(wkeep, x) for x in (wt.off, wt.slot, wt.cpu, wt.mem, wt.gpu)))
+            wh_start = _pinned(wkeep, np.zeros(wj.j, np.int32))
+
+        def step_weak():
+            weng.load_nodes(wh_nodes)
+            if tl:
+                weng.load_timeline(wh_tl)
+                return weng.place_tl(wh_jobs, node=wh_out, start=wh_start)[2]
+            return weng.place(wh_jobs, kmax=1, out=wh_out)[1]
+
+        wel, _ = timed(step_weak)
+        weng.close()
+        line["weak_scaling"] = {"value": round(wj.j * a.steps / wel * world, 1), "unit": "placements/s",
+                                "ms_per_step": round(wel / a.steps * 1e3, 3), "scaling": "weak",
+                                "per_gpu": {"nodes": wn.n, "jobs": wj.j},
+                                "parallelism": f"{world} independent cluster shards (one per GPU, no "
+                                               "data-path collective)"}
+    else:
+        eng.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

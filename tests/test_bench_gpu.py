@@ -1,6 +1,6 @@
 """bench.py keeps the driver's contract: one JSON line with the required keys, the roofline and
-CPU-baseline objects, for the C3 headline, the C5 and c3o workloads; N>1 weak scaling rehearsed with two
-ranks on one GPU (gloo for the timing collectives)."""
+CPU-baseline objects, for the C3 headline, the C5 and c3o workloads; N>1 rehearsed with two ranks on
+one GPU (gloo for the timing collectives; the strong split exchanges through the host)."""
 import json
 import os
 import socket
@@ -44,3 +44,21 @@ def test_bench_two_rank_rehearsal():
              "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse", "--scaling", "weak"])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["config"]["jobs"] == 2_000_000 and d["config"]["per_gpu"]["jobs"] == 1_000_000
+
+
+@pytest.mark.parametrize("shard_mode,workload", [("auto", "c3"), ("nodes", "c2")])
+def test_bench_two_rank_strong_rehearsal(shard_mode, workload):
+    """N > 1 default (strong: ONE C3 placement split over the ranks) rehearsed with two ranks on
+    one GPU (host exchange over gloo instead of RCCL), plus the extra `weak_scaling` leg."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    d = run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+             "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse",
+             "--shard-mode", shard_mode, "--workload", workload, "--no-device-path"])
+    jobs = 1_000_000 if workload == "c3" else 65_536
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["jobs"] == jobs
+    assert ("component" in d["config"]["parallelism"]) == (shard_mode == "auto")
+    w = d["weak_scaling"]
+    assert w["scaling"] == "weak" and w["value"] > 0 and w["per_gpu"]["jobs"] == jobs
+
