@@ -99,11 +99,12 @@ constexpr int TL_HEAD = 4;  // runs of each node copied into its header (the sca
 // Per-node header of a run list, 96 B, contiguous over nodes (the scan streams it): run count,
 // the largest free value of each column over the timeline as built (reservations only lower
 // values, so it stays an upper bound: a job whose demand exceeds it can never fit the node),
-// partition mask, and a copy of the first TL_HEAD runs.
+// partition mask, node id, and a copy of the first TL_HEAD runs.
 struct alignas(32) TlHdr {
     int32_t cnt, cpu, mem, gpu;
     uint32_t mask;
-    int32_t pad[3];
+    int32_t orig;  // node id in the caller's order (so a new dirty node needs no perm[] load)
+    int32_t pad[2];
     Seg head[TL_HEAD];
 };
 

@@ -186,7 +186,8 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
         h.gpu = max(h.gpu, sg[k].gpu);
     }
     h.mask = mask[x];
-    h.pad[0] = h.pad[1] = h.pad[2] = 0;
+    h.orig = x;
+    h.pad[0] = h.pad[1] = 0;
     for (int k = 0; k < TL_HEAD; ++k) h.head[k] = k < n ? sg[k] : Seg{H, -1, -1, -1};
     hdr[i] = h;
 }
@@ -612,7 +613,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
         const uint32_t cpos = cw != KEY_INF ? ((uint32_t)cw & TL_POS_MASK) : (uint32_t)P.nb;
         const TlHdr ch = hdr[cpos + z];
         const Seg crun = slab[(int64_t)cpos * TL_MAX_SLOTS + lane];
-        const int32_t corig = perm[cpos + z];
+        const int32_t corig = ch.orig;
         TL_CLK(c1);
         TL_ACC(0, c0, c1);
         // LDS lists: a start at slot 0 through the prefix minima — k = the first run ending at or
@@ -726,6 +727,10 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                     Seg* dst = lr + l * R;
                     if (lane < n0) dst[lane] = crun;  // n0 <= R <= 64
                     tl_pm_build(dst, pmr + l * R, n0);
+                }
+                {
+                    TL_CLK(c3h);
+                    TL_ACC(11, c3, c3h);  // header + runs wait, LDS copy, prefix minima
                 }
                 const int32_t o0 = corig;
 #pragma unroll

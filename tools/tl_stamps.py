@@ -26,6 +26,7 @@ j = max(tot[5], 1)
 names = ["clean", "dirty-eval", "new-dirty", "reserve", "tail"]
 print("cycles/job: " + ", ".join(f"{n} {tot[i] / j:.0f}" for i, n in enumerate(names)) +
       f"; new dirty per job {tot[6] / j:.2f}; write-back per job {tot[7] / j:.0f}; jobs {tot[5]}")
+print(f"new-dirty: header/runs wait + LDS copy + prefix minima {tot[11] / max(tot[6], 1):.0f} cycles per new dirty node")
 print(f"dirty-eval split: fast {tot[8] / j:.0f}, walk {tot[9] / j:.0f} (walks per job {tot[10] / j:.2f}), "
       f"reduce {(tot[1] - tot[8] - tot[9]) / j:.0f}")
 sc = buf[64 * 12:64 * 12 + 8]
