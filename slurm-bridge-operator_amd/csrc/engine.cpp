@@ -603,6 +603,7 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
         bool any = false;
         for (int k = 0; k < C; ++k) {
             CompPlan& P = c->h_plan.p[k];
+            P.k0 = 0;
             memset(&P, 0, sizeof P);
             P.nb = c->nb[k];
             P.ne = c->nb[k + 1];
@@ -861,6 +862,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
         bool any = false;
         for (int k = 0; k < C; ++k) {
             CompPlan& P = c->h_plan.p[k];
+            P.k0 = 0;
             memset(&P, 0, sizeof P);
             P.nb = c->nb[k];
             P.ne = c->nb[k + 1];

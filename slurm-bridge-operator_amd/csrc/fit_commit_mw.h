@@ -38,9 +38,13 @@
 // the counter is already drained, so the protocol costs no cycles on the decider's chain.
 #pragma once
 #include "fit_common.h"
+#include "fit_engine_ctl.h"
 
 namespace fitgpu {
 
+#ifndef MW_DTRIM
+#define MW_DTRIM 1  // 1: compile-time record slot, lane-E-only bookkeeping stores (see mw_decide)
+#endif
 #ifndef MW_ITEMS
 #define MW_ITEMS 8
 #endif
@@ -96,7 +100,8 @@ struct alignas(16) MwShared {
     uint32_t halt;     // decider stopped
     uint32_t fail;     // helper / decider watchdog
     int32_t res[4];    // CommitResult of the window
-    uint32_t pad[8];
+    uint32_t pubt;     // job tiles of the window published to the task ring (MwTiles::ring)
+    uint32_t pad[7];
     MwRec rec[MW_R];
     MwRow rows[UCAP];
     MwRow sink_rows[64];   // targets of the decider's lanes that do not write a dirty row
@@ -145,7 +150,18 @@ __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_
 struct MwTiles {
     const unsigned* tdone;  // per-tile completed slice counts of this component's window
     unsigned need;          // nslice
+    // just-in-time publishing (k_engine, ENGINE_AHEAD > 0): the committer publishes the window's
+    // first ENGINE_AHEAD job tiles; a helper that moves on to tile k publishes the tiles up to
+    // k + ENGINE_AHEAD - 1 first.  ring == nullptr: every tile was published up front.
+    unsigned long long* ring;
+    EngineCtl* ctl;
+    unsigned round;  // task round tag
+    unsigned comp;
+    unsigned ntj;    // job tiles of the window
 };
+#ifndef ENGINE_AHEAD
+#define ENGINE_AHEAD 4  // 0: every tile of the window published up front
+#endif
 
 // global address-space views of the helper's buffers: a plain (generic) pointer in a non-inlined
 // function compiles to flat loads, which also count in lgkmcnt — every LDS wait would then drain
@@ -355,10 +371,34 @@ __device__ __forceinline__ int32_t readlane(int32_t v, int l) { return __builtin
 
 // Wait until job tt's scan tile is complete (uniform; `ready` = tiles known complete, they finish
 // roughly in order).  false: the decider halted / a watchdog tripped.
+// Publish the window's job tiles [pubt, upto) (uniform; lane 0 claims the range by an LDS CAS).
+__device__ __noinline__ void mw_publish(const MwTiles& T, MwShared* S, unsigned upto) {
+    const int lane = threadIdx.x & 63;
+    unsigned from = upto;  // nothing claimed
+    if (lane == 0) {
+        unsigned cur = lds_ld(&S->pubt);
+        while (cur < upto) {  // a failed exchange reloads cur
+            if (__hip_atomic_compare_exchange_strong(&S->pubt, &cur, upto, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                from = cur;
+                break;
+            }
+        }
+    }
+    from = (unsigned)__builtin_amdgcn_readlane((int)from, 0);
+    if (from >= upto) return;
+    // claimed [from, upto): the round's plan, bounds and tile counters were released by the
+    // committer wave before the block barrier; release again from this wave before the tasks
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    engine_publish(T.ctl, T.ring, from, upto, T.need, T.round, T.comp);
+}
+
 __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& ready, MwShared* S) {
     if (!T.tdone) return true;
     const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
     if (tile < ready) return true;
+    if (T.ring && (unsigned)tile + ENGINE_AHEAD > lds_ld(&S->pubt))
+        mw_publish(T, S, min((unsigned)tile + ENGINE_AHEAD, T.ntj));
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
             T.need)
@@ -408,6 +448,54 @@ __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
             for (int i = r & 1; i + 1 < N; i += 2) mw_cas(q[i], q[i + 1]);
     }
 }
+
+// Extraction of the record's items: the nmax_ smallest tagged entries, one wave minimum each.
+#ifndef MW_XS
+#define MW_XS 1  // 0: the extraction loop with one wave minimum in SGPRs per item (round-1 design)
+#endif
+#if MW_XS
+// straight-line: each minimum lands in every lane (DPP row minima, then the permlane16 / 32
+// swaps of gfx950), so no VALU -> SGPR -> SALU hand-off or branch sits on the helper's chain;
+// all MW_M rounds run, the ones past nmax_ (or past the last entry) take nothing
+__device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
+    v = dpp_min32<0xb1>(v);
+    v = dpp_min32<0x4e>(v);
+    v = dpp_min32<0x141>(v);
+    v = dpp_min32<0x140>(v);  // every lane: its row's minimum
+    {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = min((uint32_t)p[0], (uint32_t)p[1]);
+    }
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return min((uint32_t)p[0], (uint32_t)p[1]);
+}
+#define MW_EXTRACT                                                                             \
+        _Pragma("unroll") for (int i_ = 0; i_ < MW_M; ++i_) {                                  \
+            const uint32_t hh_ = (uint32_t)(q_[0] >> 32), ll_ = (uint32_t)q_[0];              \
+            const uint32_t mh_ = wave_min32_all(hh_);                                          \
+            const uint32_t ml_ = wave_min32_all(hh_ == mh_ ? ll_ : 0xffffffffu);               \
+            const bool take_ = i_ < nmax_ && (mh_ & ml_) != 0xffffffffu;                       \
+            const bool me_ = take_ && hh_ == mh_ && ll_ == ml_; /* tagged keys are unique */   \
+            n_ += take_ ? 1 : 0;                                                               \
+            sel_ = me_ ? sel_ | ((uint32_t)(i_ + 1) << (4u * (ml_ & 7u))) : sel_;              \
+            _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
+                q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
+            q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
+        }                                                                                      \
+        n_ = rfl(n_);
+#else
+#define MW_EXTRACT                                                                             \
+        for (; n_ < nmax_; ++n_) {                                                             \
+            const uint64_t best_ = wave_min64_2pass(q_[0]);                                    \
+            if (best_ == KEY_INF) break;                                                       \
+            const bool me_ = q_[0] == best_; /* tagged keys are unique */                      \
+            const uint32_t sv_ = (uint32_t)(n_ + 1) << (4u * ((uint32_t)best_ & 7u));          \
+            sel_ = me_ ? sel_ | sv_ : sel_;                                                    \
+            _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
+                q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
+            q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
+        }
+#endif
 
 // Helper h (1..MW_H) pre-resolves jobs t = h-1, h-1+H, ...  Loads run two jobs ahead (keys, job
 // row, bound) and one job ahead (the node rows of the candidates); the three register sets are
@@ -502,23 +590,11 @@ __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
         _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) q_[e] = mw_tag(x0[e], e);           \
         _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) q_[MW_EPL + i] = mw_tag(xd[i], MW_EPL + i);\
         mw_sort(q_);                                                                           \
-        /* item index + 1 of each entry, 4 bits per entry (0: not taken); depth = entries this  \
-           lane gave (a prefix of its sorted list) */                                          \
+        /* item index + 1 of each entry, 4 bits per entry (0: not taken) */                     \
         uint32_t sel_ = 0u;                                                                    \
-        int depth_ = 0;                                                                        \
         /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */  \
         const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
-        for (; n_ < nmax_; ++n_) {                                                             \
-            const uint64_t best_ = wave_min64_2pass(q_[0]);                                    \
-            if (best_ == KEY_INF) break;                                                       \
-            const bool me_ = q_[0] == best_; /* tagged keys are unique */                      \
-            const uint32_t sv_ = (uint32_t)(n_ + 1) << (4u * ((uint32_t)best_ & 7u));          \
-            sel_ = me_ ? sel_ | sv_ : sel_;                                                    \
-            depth_ += me_;                                                                     \
-            _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
-                q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
-            q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
-        }                                                                                      \
+        MW_EXTRACT                                                                             \
         /* items: the lanes that gave an entry store it (exec-masked: only those lanes use   \
            the LDS, which the decider shares) */                                               \
         _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) {                                   \
@@ -707,7 +783,13 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
     // ready word of record t+1 (relaxed; acquired below, before its data is read)
+#if MW_DTRIM
+    // t == E (mod 8) while the window runs (each window starts at t = 0 and every step before an
+    // exit advances t by one; after an exit the record read below is never used)
+    const MwRec* Rn = &S->rec[(E + 1) & (MW_R - 1)];
+#else
     const MwRec* Rn = &S->rec[(t + 1) & (MW_R - 1)];
+#endif
     const uint32_t flag_n = lds_ld(&Rn->h.ready);
     MW_SEG(D, 1);
 
@@ -829,6 +911,32 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     MW_SEG(D, 5);
     // bookkeeping: dirty row, bitmap bit — fire-and-forget LDS writes from lane E (the other
     // lanes write their own sink words: no exec masking, no branch)
+#if MW_DTRIM
+    // lane E alone (exec = its bit, or none when the job is not placed) stores the new row and ORs
+    // the bitmap bit (0 when the node was already dirty): 3 LDS ops of one lane instead of 64
+    // lanes' worth of sink traffic in the LDS pipe the helpers share
+    {
+        typedef __attribute__((address_space(3))) MwRow* LRow;
+        const uint32_t ra = (uint32_t)(uintptr_t)(LRow)&S->rows[slot];
+        const uint32_t rel = (uint32_t)pos - (uint32_t)P.nb;
+        const uint32_t ba = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&S->bitmap[rel >> 5];
+        const uint32_t bv = fresh ? 1u << (rel & 31) : 0u;
+        const uint32_t pl = (uint32_t)rfl(placed ? 1 : 0);
+        const uint64_t m = ((uint64_t)(uint32_t)rfl((int32_t)(pl << E)) |
+                            ((uint64_t)(uint32_t)rfl(0) << 32));  // exec mask: SGPR pair
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %[sv], exec\n\t"
+            "s_mov_b64 exec, %[m]\n\t"
+            "ds_write_b128 %[ra], %[a]\n\t"
+            "ds_write_b128 %[ra], %[b] offset:16\n\t"
+            "ds_or_b32 %[ba], %[bv]\n\t"
+            "s_mov_b64 exec, %[sv]"
+            : [sv] "=&s"(sv)
+            : [m] "s"(m), [ra] "v"(ra), [a] "v"(R.a), [b] "v"(R.b), [ba] "v"(ba), [bv] "v"(bv)
+            : "memory");
+    }
+#else
     {
         const bool me = lane == E && placed;
         MwRow* dst = me ? &S->rows[slot] : &S->sink_rows[lane];
@@ -845,6 +953,7 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                               __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
     }
+#endif
     D.nu += fresh;
     D.placed += placed;
     MW_SEG(D, 6);
@@ -941,7 +1050,7 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
                                                          const uint64_t* __restrict__ bnd,
                                                          const JobRec* __restrict__ wjob,
                                                          int32_t* __restrict__ out, int kmax,
-                                                         MwTiles T = MwTiles{nullptr, 0u}) {
+                                                         MwTiles T = MwTiles{nullptr, 0u, nullptr, nullptr, 0u, 0u, 0u}) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;

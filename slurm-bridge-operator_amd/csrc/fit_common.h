@@ -153,7 +153,11 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
 // bitonic tree, giving the exact top-K (and bound) of the block-slice.  K = P.ks (KS, or fewer
 // keys over more block-slices for a large component: the same candidates per job, but a round's
 // first job tile — which the commit waits for — is spread over more blocks).
-template <bool PERSISTENT, int K>
+// KW > K (the persistent engine's first job tile of a round, FIT_K0): keep only the top-K per
+// block-slice but write the plan's KW-entry layout, padded with KEY_INF — an exact (list, bound)
+// pair of K entries, whose insertion network is KW / K times cheaper than the full list's: the
+// tile the commit waits for at every round start arrives sooner.
+template <bool PERSISTENT, int K, int KW = K>
 __device__ __forceinline__ void scan_tile(
     const CompPlan& P, int tile, int s, const NodeRec* __restrict__ rec,
     const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
@@ -213,12 +217,12 @@ __device__ __forceinline__ void scan_tile(
         __syncthreads();
     }
     if (wave != 0 || !active) return;  // (no barrier follows inside scan_tile)
-    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * K;
+    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KW;
 #pragma unroll
-    for (int i = 0; i < K; i += 2) {
+    for (int i = 0; i < KW; i += 2) {
         ulonglong2 v;
-        v.x = key[i];
-        v.y = key[i + 1];
+        v.x = i < K ? key[i] : KEY_INF;
+        v.y = i + 1 < K ? key[i + 1] : KEY_INF;
         *reinterpret_cast<ulonglong2*>(dst + i) = v;
     }
     if (key[K - 1] != KEY_INF)

@@ -59,6 +59,7 @@ struct alignas(16) CompPlan {
     int32_t ks;          // keys kept per (job, block-slice): KS, or fewer for a large component
     int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
     int32_t slot0;       // first window slot (global over components)
+    int32_t k0;          // persistent engine: the round's first job tile may keep FIT_K0 keys (k = 1 window)
 };
 
 // Persistent engine (fit_persistent.hip): per-component state written by the host, results

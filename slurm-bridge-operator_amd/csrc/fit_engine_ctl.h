@@ -55,6 +55,26 @@ __device__ __forceinline__ void engine_round_finished(EngineCtl* ctl, int c, uns
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Publish job tiles [from, upto) of component c's window (every block-slice of each) to the task
+// ring: one wave, uniform arguments.  The caller has released (agent scope) what the tasks'
+// scans read — the round's plan, bound / tile-counter resets and node state.
+__device__ __forceinline__ void engine_publish(EngineCtl* ctl, unsigned long long* ring,
+                                               unsigned from, unsigned upto, unsigned nslice,
+                                               unsigned round, unsigned c) {
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned n = (upto - from) * nslice;
+    unsigned base = 0;
+    if (lane == 0)
+        base = __hip_atomic_fetch_add(&ctl->q_tail, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
+    for (unsigned i = lane; i < n; i += 64) {
+        const unsigned idx = base + i;
+        const unsigned tile = from + i / nslice, sl = i % nslice;
+        __hip_atomic_store(ring + (idx & (QCAP - 1)), engine_task(idx / QCAP + 1, round, tile, sl, c),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __device__ __forceinline__ void acquire_agent() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -77,6 +77,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // handles k > 1) after its whole scan; the decider/helper pipeline covers k = 1
             // windows and starts at once: helpers wait per job tile (MwTiles)
             const bool multi = jpk[cursor + w] != jpk[cursor];
+            P.k0 = multi ? 0 : 1;  // a multi-node job needs k <= KS keys in its first tile
             if (wave == 0) {
                 t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                 // the previous round's tiles (also those past its stop) must all be complete
@@ -88,24 +89,24 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 release_agent();  // plan, bound / counter reset and last round's node rows → visible
-                const unsigned ntiles = ntj * (unsigned)S.nslice;
-                unsigned base = 0;
-                if (lane == 0)
-                    base = __hip_atomic_fetch_add(&ctl->q_tail, ntiles, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                base = __builtin_amdgcn_readfirstlane(base);
-                for (unsigned i = lane; i < ntiles; i += 64) {
-                    const unsigned idx = base + i;
-                    const unsigned tile = i / S.nslice, sl = i - tile * S.nslice;
-                    const unsigned long long g =
-                    engine_task(idx / QCAP + 1, (unsigned)rounds + 1u, tile, sl, (unsigned)c);
-                    __hip_atomic_store(ring + (idx & (QCAP - 1)), g, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-                target += ntiles;
+                // just-in-time publishing (ENGINE_AHEAD > 0, k = 1 windows): the first
+                // ENGINE_AHEAD job tiles now, the rest by the helpers as they reach them
+                // (fit_commit_mw.h mw_publish), so the ring never holds a whole window of tiles
+                // that a new round's first tile would queue behind — and the tiles past a stop
+                // are never scanned
+                const unsigned npub = (ENGINE_AHEAD > 0 && !multi) ? min(ntj, (unsigned)ENGINE_AHEAD) : ntj;
+                if (lane == 0) M->pubt = npub;
+                const unsigned ntiles = npub * (unsigned)S.nslice;
 #ifdef FIT_STAMPS
-                if (lane == 0) ctl->pub[c] = __builtin_amdgcn_s_memrealtime();
+                // before the tasks turn visible: a worker may pick tile 0 at once
+                if (lane == 0) {
+                    __hip_atomic_store(&ctl->pub[c], __builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                }
 #endif
+                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                if (npub == ntj) target += ntiles;  // else: after the commit (M->pubt)
                 if (multi && !fail) fail = !wait_tiles(ctl, c, target);
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // node rows written by this block: CU-wide view for all waves
@@ -118,8 +119,15 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // handles k > 1); the decider/helper pipeline covers k = 1 windows
             CommitResult R;
             if (!multi) {
+                const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
+                const bool jit = ENGINE_AHEAD > 0 && M->pubt < ntj;  // block-uniform (before the barrier)
                 R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax,
-                                     MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice});
+                                     MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
+                                             jit ? ring : nullptr, ctl,
+                                             (unsigned)rounds + 1u, (unsigned)c, ntj});
+                // every tile published this round (the committer's and the helpers') must be
+                // complete before the next round reuses the buffers: count them
+                if (jit && wave == 0) target += M->pubt * (unsigned)S.nslice;
             } else {
                 if (wave == 0) {
                     const CommitResult r0 =
@@ -217,11 +225,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
             const CompPlan P = plans[c];
+#ifndef FIT_K0
+#define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
+#endif
             switch (P.ks) {  // block-uniform; the host picks one of these (engine.cpp)
 #define SCAN_K(K_)                                                                               \
     case K_:                                                                                      \
-        scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd,   \
-                            wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem));                   \
+        if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0)                                             \
+            scan_tile<true, (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_), K_>(                       \
+                P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,         \
+                reinterpret_cast<uint64_t(*)[(FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_)][64]>(smem)); \
+        else                                                                                      \
+            scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand,    \
+                                bnd, wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem));          \
         break;
                 SCAN_K(16)
                 SCAN_K(8)
