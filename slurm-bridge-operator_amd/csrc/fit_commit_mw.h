@@ -431,11 +431,15 @@ __device__ __forceinline__ void mw_cas(uint64_t& a, uint64_t& b) {
     a = lo;
     b = hi;
 }
-// ascending sort of a lane's entries (static indices only): the 12-comparator network for 6,
-// odd-even transposition otherwise
+// ascending sort of a lane's entries (static indices only): the optimal networks for 4 (5
+// comparators) and 6 (12), odd-even transposition otherwise
 template <int N>
 __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
-    if constexpr (N == 6) {
+    if constexpr (N == 4) {
+        mw_cas(q[0], q[1]); mw_cas(q[2], q[3]);
+        mw_cas(q[0], q[2]); mw_cas(q[1], q[3]);
+        mw_cas(q[1], q[2]);
+    } else if constexpr (N == 6) {
         mw_cas(q[0], q[5]); mw_cas(q[1], q[3]); mw_cas(q[2], q[4]);
         mw_cas(q[1], q[2]); mw_cas(q[3], q[4]);
         mw_cas(q[0], q[3]); mw_cas(q[2], q[5]);
