@@ -64,7 +64,8 @@ static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
 constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
-#define MW_HSLEEP 12  // helper back-off per missing decided job, in units of 64 cycles
+#define MW_HSLEEP 1  // helper back-off per missing decided job, in units of 64 cycles (12 before the
+                      // 4-entry helpers: C3 k_engine 32.2 -> 31.2 ms at 0-2)
 #endif
 constexpr int MW_EPL = (MAX_SLICES * KS + 63) / 64;  // candidate entries per helper lane
 static_assert(MW_EPL <= 2, "at most two candidate entries per lane");
