@@ -8,6 +8,9 @@ namespace fitgpu {
 #define FIT_KS 16
 #endif
 constexpr int KS = FIT_KS;      // candidates kept per (job, block-slice) by fit_scan
+// the per-wave insertion network and the LDS bitonic merge tree of k_scan need a power of two
+// (a FIT_KS=12 build placed jobs wrongly before this check)
+static_assert(KS >= 2 && KS <= 64 && (KS & (KS - 1)) == 0, "FIT_KS must be a power of two in [2, 64]");
 constexpr int SCAN_WAVES = 8;   // waves per scan block; each walks one sub-slice of nodes
 constexpr int SCAN_JOBS = 64;   // jobs per scan block (lanes = jobs, shared by the 8 waves)
 #ifndef FIT_MIN_SUB
@@ -22,6 +25,7 @@ constexpr int MAX_SLICES = FIT_MAX_SLICES;  // block-slices per job per rank (su
 #define FIT_TL_KS 4
 #endif
 constexpr int TL_KS = FIT_TL_KS;  // candidates per (job, block-slice) of the backfill scan
+static_assert(TL_KS >= 1 && TL_KS <= 64 && (TL_KS & (TL_KS - 1)) == 0, "FIT_TL_KS must be a power of two");
 #ifndef FIT_UCAP
 #define FIT_UCAP 128  // 256: fewer dirty-full stops, but 6 helper entries per lane instead of 4
 #endif                 // (C3 k_engine 33.6 -> 32.3 ms at 128, C2 -4 %, C3o +2 %)
