@@ -19,6 +19,9 @@
 namespace fitgpu {
 
 constexpr int TL_PM_STEPS = 32;     // LDS run lists hold <= 2 * TL_PM_STEPS = 64 runs
+#ifndef TL_PAD
+#define TL_PAD 1  // runs of padding between two lanes' LDS run-list regions (0: packed, bank-conflicted)
+#endif
 constexpr int TL_UPL = TL_UCAP / 64;  // dirty slots per lane
 #ifndef TL_WAVE_WALKS
 #define TL_WAVE_WALKS 12 // walking LDS lists up to which a job walks them one at a time wave-wide
@@ -506,9 +509,14 @@ __device__ __forceinline__ CommitResult commit_tl_window(
     const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
     int32_t H, int32_t R, const unsigned* tdone = nullptr, unsigned need = 0) {
     Seg* scr = reinterpret_cast<Seg*>(smem);                // general-path scratch
-    Seg* lr = scr + TL_MAX_SLOTS;                           // TL_UCAP regions of R runs
-    int4* pmr = reinterpret_cast<int4*>(lr + TL_UCAP * R);  // their prefix minima
-    uint32_t* bitmap = reinterpret_cast<uint32_t*>(pmr + TL_UCAP * R);
+    // TL_UCAP regions of R runs, TL_PAD runs apart beyond R: a lane's region starts 16 B further
+    // along the banks than its neighbour's, so the lanes' reads of their own lists (the 4-ary
+    // search, the prefix-minimum read) spread over the banks instead of all hitting one (a
+    // 1,024-B stride maps every lane of a ds_read_b32 group to the same bank: 32-way)
+    const int32_t RS = R > 0 ? R + TL_PAD : 0;  // no regions when R = 0 (every list global)
+    Seg* lr = scr + TL_MAX_SLOTS;
+    int4* pmr = reinterpret_cast<int4*>(lr + TL_UCAP * RS);  // their prefix minima
+    uint32_t* bitmap = reinterpret_cast<uint32_t*>(pmr + TL_UCAP * RS);
     const int lane = threadIdx.x & 63;
     if (P.w == 0) return CommitResult{0, 0, 0, 0};
     const int nwords = (P.ne - P.nb + 31) >> 5;
@@ -628,7 +636,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
             dk[i] = KEY_INF;
             walk[i] = dl && uglob[i];
             if (dl && !uglob[i]) {
-                const Seg* const mine = lr + (i * 64 + lane) * R;
+                const Seg* const mine = lr + (i * 64 + lane) * RS;
                 int k = 0;
 #pragma unroll
                 for (int q = 16; q >= 1; q >>= 2) {
@@ -642,7 +650,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                     const int32_t x3 = i3 < ucnt[i] ? y3 : TL_BIG;
                     k += q * ((x1 < jd) + (x2 < jd) + (x3 < jd));
                 }
-                const int4 pk = pmr[(i * 64 + lane) * R + k];
+                const int4 pk = pmr[(i * 64 + lane) * RS + k];
                 if (pk.x >= jc && pk.y >= jm && pk.z >= jg) {
                     dk[i] = tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, upos[i]);
                     fit0 = true;
@@ -676,13 +684,13 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                 uint64_t wl = KEY_INF;
                 const uint64_t mlds = __ballot(walk[i] && !uglob[i]);
                 if (__popcll(mlds) > TL_WAVE_WALKS) {
-                    wl = tl_eval4(lr + (i * 64 + lane) * R, ucnt[i], R, walk[i] && !uglob[i], jc,
+                    wl = tl_eval4(lr + (i * 64 + lane) * RS, ucnt[i], R, walk[i] && !uglob[i], jc,
                                   jm, jg, jd, H, upos[i], cutw);
                 } else for (uint64_t mwl = mlds; mwl; mwl &= mwl - 1) {
                     const int ll = __builtin_ctzll(mwl);
                     const int n = __builtin_amdgcn_readlane(ucnt[i], ll);
                     const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)upos[i], ll);
-                    const uint64_t k = tl_walk_wave(lr + (i * 64 + ll) * R, n, jc, jm, jg, jd, wlim, p);
+                    const uint64_t k = tl_walk_wave(lr + (i * 64 + ll) * RS, n, jc, jm, jg, jd, wlim, p);
                     if (lane == ll) wl = k;
                 }
                 uint64_t wg = KEY_INF;
@@ -724,9 +732,9 @@ __device__ __forceinline__ CommitResult commit_tl_window(
                 const int n0 = __builtin_amdgcn_readfirstlane(h0.cnt);
                 const bool g = n0 > R;
                 if (!g) {
-                    Seg* dst = lr + l * R;
+                    Seg* dst = lr + l * RS;
                     if (lane < n0) dst[lane] = crun;  // n0 <= R <= 64
-                    tl_pm_build(dst, pmr + l * R, n0);
+                    tl_pm_build(dst, pmr + l * RS, n0);
                 }
                 {
                     TL_CLK(c3h);
@@ -768,10 +776,10 @@ __device__ __forceinline__ CommitResult commit_tl_window(
             start = (int32_t)(best >> 54);
             int nn;
             if (!g) {
-                Seg* L = lr + l * R;
+                Seg* L = lr + l * RS;
                 nn = tl_reserve_lds(L, n, R, start, start + jd, jc, jm, jg);
                 if (nn >= 0) {
-                    tl_pm_build(L, pmr + l * R, nn);
+                    tl_pm_build(L, pmr + l * RS, nn);
                 } else {  // outgrows its LDS region: move the list to the global slab
                     Seg* gl = slab + (int64_t)pos * TL_MAX_SLOTS;
                     if (lane < n) gl[lane] = L[lane];
@@ -831,7 +839,7 @@ __device__ __forceinline__ CommitResult commit_tl_window(
         Seg* dst = slab + (int64_t)p * TL_MAX_SLOTS;
         Seg hd = Seg{H, -1, -1, -1};
         if (!gl) {
-            const Seg* src = lr + l * R;
+            const Seg* src = lr + l * RS;
             if (lane < n) {
                 hd = src[lane];
                 dst[lane] = hd;
@@ -1096,13 +1104,15 @@ constexpr size_t TL_LDS_LIMIT = 160 * 1024;
 int commit_tl_runs(int32_t max_component_nodes) {
     const size_t fixed = sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
     if (fixed >= TL_LDS_LIMIT) return 0;
-    return (int)std::min<size_t>(2 * TL_PM_STEPS,
-                                 (TL_LDS_LIMIT - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP));
+    const size_t fit = (TL_LDS_LIMIT - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP);
+    if (fit <= (size_t)TL_PAD) return 0;
+    return (int)std::min<size_t>(2 * TL_PM_STEPS, fit - TL_PAD);
 }
 
 size_t commit_tl_lds_bytes(int32_t max_component_nodes) {
+    const int runs = commit_tl_runs(max_component_nodes);
     return sizeof(Seg) * TL_MAX_SLOTS +
-           (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * commit_tl_runs(max_component_nodes) +
+           (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * (runs > 0 ? runs + TL_PAD : 0) +
            (size_t)((max_component_nodes + 31) / 32) * 4;
 }
 
@@ -1129,13 +1139,15 @@ constexpr size_t TL_ENGINE_LDS = 160 * 1024;
 int engine_tl_runs(int32_t max_component_nodes) {
     const size_t fixed = sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
     if (fixed >= TL_ENGINE_LDS) return 0;
-    return (int)std::min<size_t>(2 * TL_PM_STEPS,
-                                 (TL_ENGINE_LDS - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP));
+    const size_t fit = (TL_ENGINE_LDS - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP);
+    if (fit <= (size_t)TL_PAD) return 0;
+    return (int)std::min<size_t>(2 * TL_PM_STEPS, fit - TL_PAD);  // regions are R + TL_PAD apart
 }
 
 size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
+    const int runs = engine_tl_runs(max_component_nodes);
     const size_t commit = sizeof(Seg) * TL_MAX_SLOTS +
-                          (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * engine_tl_runs(max_component_nodes) +
+                          (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * (runs > 0 ? runs + TL_PAD : 0) +
                           (size_t)((max_component_nodes + 31) / 32) * 4;
     const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16;
     return std::max(commit, scan);
