@@ -92,8 +92,8 @@ def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_comm
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5"],
                     help="c3: BASELINE headline (100k x 1M); c3o: c3 + an all-nodes partition (one "
                          "component); c5: c3 with a 1,024-slot backfill horizon")

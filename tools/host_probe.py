@@ -21,6 +21,19 @@ def pinned(keep, a):
     return out.view(a.dtype) if view else out
 
 
+if "--bind" in sys.argv:  # host thread on the CPUs local to GPU 0 (intersected with what we may use)
+    import glob
+    allowed = os.sched_getaffinity(0)
+    for f in sorted(glob.glob("/sys/class/drm/card*/device/local_cpulist")):
+        txt = open(f).read().strip()
+        cpus = set()
+        for part in txt.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        print(f, txt, "allowed", len(allowed), "local&allowed", len(cpus & allowed))
+        if cpus & allowed:
+            os.sched_setaffinity(0, cpus & allowed)
+            break
 nodes, jobs, parts = synth.make_config("c3")
 keep = []
 hn = synth.Nodes(*(pinned(keep, x) for x in (nodes.cpu_free, nodes.mem_free, nodes.gpu_free, nodes.avail_min, nodes.part_mask)))
