@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 4
+#define FITGPU_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -267,18 +267,95 @@ typedef struct {
     int64_t batch;           /* batch sequence number (0, 1, ...)                           */
     int32_t batch_jobs;      /* requests placed together in that batch                      */
     int32_t order;           /* this request's index in the batch's placement order        */
+    int64_t ticket;          /* reservation id (> 0) when placed, else 0: see "reservations" */
 } fit_admit_res;
 int fit_admitter_create(fit_ctx* ctx, int32_t max_batch, int32_t max_wait_us, fit_admitter** out);
 /* Blocks until the request's batch is placed.  FIT_OK (result in *res), FIT_E_INVAL (bad
  * request: negative demand, nodes_k > FIT_MAX_K; not queued), FIT_E_STATE (admitter shutting
  * down / no node table), or the batch's fit_place error. */
 int fit_admit(fit_admitter* a, const fit_admit_req* req, fit_admit_res* res);
+/* All-or-nothing admission of n requests (the tasks of one array job, fit_pod_demand): they join
+ * ONE batch, consecutively in arrival order at their own priority.  If any of them is not placed,
+ * none is: every res[i].node[0] is FIT_REJECTED (some task violates the partition limits) or
+ * FIT_UNPLACED, ticket 0, and what the placed ones took goes back to the table before the next
+ * batch (requests after the group in the same batch saw it taken: conservative, never an
+ * over-commit).  Errors as fit_admit. */
+int fit_admit_group(fit_admitter* a, const fit_admit_req* reqs, int32_t n, fit_admit_res* res);
+/* Replaces the node table between batches (the node ticker, provider.go:470-488).  Every open
+ * reservation (admitted, neither confirmed nor released) is taken from the new table again
+ * before it is loaded — Slurm does not count a job it has not allocated yet, so a refresh would
+ * otherwise hand its capacity out twice. */
 int fit_admitter_load_nodes(fit_admitter* a, int32_t n, const int32_t* cpu_free,
                             const int32_t* mem_free, const int32_t* gpu_free,
                             const int32_t* avail_min, const uint32_t* part_mask);
 int fit_admitter_partition_free(fit_admitter* a, int32_t p, int64_t* cpu, int64_t* mem_mib,
                                 int64_t* gpu);
+/* Reservations.  A placed request holds its demand on its nodes from admission until:
+ *   confirm — Slurm now counts the job (it is allocated: the agent's Nodes RPC includes it, e.g.
+ *             the pod's job is RUNNING): the reservation is dropped at the next load, not
+ *             re-applied (the table then carries the allocation);
+ *   release — the job will not run (pod deleted, SubmitJob failed): its demand goes back to the
+ *             current table before the next batch (requires a table loaded through
+ *             fit_admitter_load_nodes, else FIT_E_STATE); a confirmed one is only forgotten;
+ *   ttl     — fit_admitter_set_ttl(a, L), L > 0: an open reservation that L loads have
+ *             re-applied is dropped (a lost confirmation cannot hold capacity forever; 0 = never).
+ * FIT_E_INVAL: unknown ticket. */
+int fit_admitter_confirm(fit_admitter* a, int64_t ticket);
+int fit_admitter_release(fit_admitter* a, int64_t ticket);
+int fit_admitter_set_ttl(fit_admitter* a, int32_t loads);
+/* Open reservations / requests queued for the next batch (monitoring, tests). */
+int fit_admitter_reservations(fit_admitter* a);
+int fit_admitter_pending(fit_admitter* a);
 void fit_admitter_destroy(fit_admitter* a);
+
+/* ---- CreatePod call site -------------------------------------
+ * What the virtual kubelet's CreatePod has in hand — the pod's sbo.kubecluster.org/<key> labels
+ * (newSubmitRequestForPod, pkg/slurm-virtual-kubelet/provider.go:62-125; keys
+ * pkg/common/labels.go:9-14) and its sbatch script (Containers[0].Command[0], provider.go:71) —
+ * turned into engine requests, and the engine's decision written back into the script. */
+typedef struct {
+    const char* nodes;            /* sbo.kubecluster.org/nodes            (NULL = label absent) */
+    const char* cpus_per_task;    /* sbo.kubecluster.org/cpus-per-task                          */
+    const char* mem_per_cpu;      /* sbo.kubecluster.org/mem-per-cpu                            */
+    const char* ntasks_per_node;  /* sbo.kubecluster.org/ntasks-per-node                        */
+    const char* array;            /* sbo.kubecluster.org/array                                  */
+    const char* ntasks;           /* sbo.kubecluster.org/ntask                                  */
+} fit_pod_labels;
+/* Slurm --array expression ("0-15", "1,3,5-7", "0-15:4", "1-100%10") → the number of distinct
+ * task ids and how many may run at once (min(tasks, %limit)).  The fix of parseArrayLen
+ * (pkg/slurm-bridge-operator/parse.go:126-135), which gives 0 for "1-10%2" and "1-3,5".
+ * FIT_E_PARSE: malformed, or a task id above 4,194,303. */
+int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running);
+/* The pod's demand as sbatch sees it: the script's #SBATCH header (extractBatchResourcesFromScript,
+ * parse.go:30-69: --time, --nodes, --mem-per-cpu, --cpus-per-task, --ntasks-per-node), overridden
+ * by the labels (they reach sbatch as command-line flags, pkg/slurm-agent/slurm.go:189-229; a
+ * value strconv.ParseInt rejects is skipped, as provider.go:74-123 logs and skips it), then the
+ * operator's defaults (pod.go:97-107) and fit_job_demand's per-node rule.  An array job becomes
+ * one request per task that may run at once (fit_array_tasks; each task runs on its own nodes).
+ * Writes min(n, cap) requests (partition `part`, priority `priority`) and returns n >= 1, or
+ * FIT_E_PARSE (malformed #SBATCH header or array) / FIT_E_INVAL (demand out of range). */
+int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
+                   int64_t priority, fit_admit_req* out, int32_t cap);
+/* The script with `#SBATCH --nodelist=<names of node[0..k)>` added as the last line of its
+ * #SBATCH header (after the last header line, so it overrides an earlier --nodelist / -w and the
+ * header stays contiguous for extractBatchResourcesFromScript), so slurmctld allocates the nodes
+ * the engine reserved — SubmitJobRequest.script (workload.proto:66), no proto change.  names: the
+ * node table's names, NUL-separated in node-id order (fit_ingest_nodes, or the Partition RPC's
+ * list), n_names of them.  Returns the length written (NUL-terminated), FIT_E_INVAL (a node id
+ * out of range, or out too small: it needs strlen(script) + 32 + Σ (strlen(name) + 1)). */
+int fit_script_with_nodelist(const char* script, const char* names, int32_t n_names,
+                             const int32_t* node, int32_t k, char* out, int32_t outlen);
+/* ResourcesResponse (workload.proto:137-148, filled by pkg/slurm-agent/api/slurm.go:297-341:
+ * wallTime in seconds, 0 when UNLIMITED; cpuPerNode / memPerNode, -1 or 0 when unlimited or
+ * unset) → fit_load_partitions' limits (minutes rounded up, -1 = no limit). */
+int fit_partition_limits(int64_t wall_time_s, int64_t cpu_per_node, int64_t mem_per_node,
+                         int32_t* max_time_min, int32_t* max_cpus_per_node,
+                         int32_t* max_mem_per_node);
+/* NodesResponse rows (workload.proto:165-174, as fit_node) → fit_load_nodes columns: free =
+ * total − alloc clamped to int32, avail_min = INT32_MAX, part_mask for every row. */
+int fit_node_columns(const fit_node* nodes, int32_t n, uint32_t part_mask, int32_t* cpu_free,
+                     int32_t* mem_free, int32_t* gpu_free, int32_t* avail_min,
+                     uint32_t* mask);
 
 #ifdef __cplusplus
 }

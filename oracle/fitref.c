@@ -464,6 +464,148 @@ void ref_pod_request(const ref_job_resources* r, int64_t* cpu, int64_t* memory) 
     *memory = (int64_t)(c * (uint64_t)r->mem_per_cpu * 1024u);
 }
 
+/* DESIGN.md §2 "demand": the engine's per-node request of one (task of a) job.  Restated from the
+ * SPEC text, not from the product: k = nodes (>= 1); tasks per node = ntasksPerNode, else
+ * ceil(ntasks / k), else 1; cpu = cpusPerTask x tasks per node; mem = cpu x memPerCpu (MiB);
+ * wall = walltime rounded up to whole minutes.  -1: a value outside the engine's int32 / k range. */
+int ref_job_demand(const ref_job_resources* r, int32_t* cpu, int32_t* mem, int32_t* wall,
+                   uint16_t* k) {
+    int64_t nodes = r->nodes >= 1 ? r->nodes : 1;
+    int64_t per_node_tasks = 1;
+    if (r->ntasks_per_node >= 1)
+        per_node_tasks = r->ntasks_per_node;
+    else if (r->ntasks >= 1)
+        per_node_tasks = r->ntasks / nodes + (r->ntasks % nodes != 0);
+    int64_t cpt = r->cpus_per_task >= 1 ? r->cpus_per_task : 1;
+    int64_t mpc = r->mem_per_cpu >= 1 ? r->mem_per_cpu : 1024;
+    if (nodes > 65535 || r->wall_ns < 0) return -1;
+    /* overflow-safe products against INT32_MAX */
+    if (per_node_tasks > INT32_MAX / cpt) return -1;
+    int64_t c = per_node_tasks * cpt;
+    if (mpc > INT32_MAX / c + 1 || c * mpc > INT32_MAX) return -1;
+    int64_t minutes = r->wall_ns / NS_PER_MIN + (r->wall_ns % NS_PER_MIN != 0);
+    if (minutes > INT32_MAX) return -1;
+    *cpu = (int32_t)c;
+    *mem = (int32_t)(c * mpc);
+    *wall = (int32_t)minutes;
+    *k = (uint16_t)nodes;
+    return 0;
+}
+
+static int cmp_i64(const void* a, const void* b) {
+    int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return (x > y) - (x < y);
+}
+
+static int all_digits(const char* s, size_t n) {
+    if (n == 0) return 0;
+    for (size_t i = 0; i < n; i++)
+        if (s[i] < '0' || s[i] > '9') return 0;
+    return 1;
+}
+
+/* Slurm's --array syntax (sbatch(1) "--array=<indexes>": comma-separated ids and ranges "a-b",
+ * ranges with a step "a-b:s", an optional "%N" limit on simultaneously running tasks).  The
+ * ids are listed explicitly, sorted and de-duplicated here.  -1: malformed / id > 4194303. */
+int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running) {
+    span a = trim_space(array, strlen(array));
+    int64_t limit = -1;
+    const char* pct = memchr(a.p, '%', a.n);
+    size_t body = a.n;
+    if (pct) {
+        size_t off = (size_t)(pct - a.p) + 1;
+        if (!all_digits(a.p + off, a.n - off) || go_parse_int(a.p + off, a.n - off, &limit) || limit < 1)
+            return -1;
+        body = (size_t)(pct - a.p);
+    }
+    if (body == 0) return -1;
+    size_t cap = 1024, cnt = 0;
+    int64_t* ids = malloc(cap * sizeof *ids);
+    if (!ids) return -1;
+    size_t i = 0;
+    int bad = 0;
+    while (i <= body && !bad) {
+        size_t j = i;
+        while (j < body && a.p[j] != ',') j++;
+        /* item [i, j): lo[-hi[:step]] */
+        const char* it = a.p + i;
+        size_t n = j - i;
+        const char* d = memchr(it, '-', n);
+        const char* c = memchr(it, ':', n);
+        int64_t lo, hi, st = 1;
+        size_t nlo = d ? (size_t)(d - it) : (c ? (size_t)(c - it) : n);
+        if (c && !d) bad = 1;
+        if (!bad && (!all_digits(it, nlo) || go_parse_int(it, nlo, &lo))) bad = 1;
+        hi = lo;
+        if (!bad && d) {
+            size_t off = nlo + 1, nhi = (c ? (size_t)(c - it) : n) - off;
+            if (!all_digits(it + off, nhi) || go_parse_int(it + off, nhi, &hi)) bad = 1;
+        }
+        if (!bad && c) {
+            size_t off = (size_t)(c - it) + 1;
+            if (!all_digits(it + off, n - off) || go_parse_int(it + off, n - off, &st) || st < 1) bad = 1;
+        }
+        if (!bad && (hi < lo || hi > 4194303)) bad = 1;
+        for (int64_t x = lo; !bad && x <= hi; x += st) {
+            if (cnt == cap) {
+                cap *= 2;
+                int64_t* g = realloc(ids, cap * sizeof *ids);
+                if (!g) {
+                    bad = 1;
+                    break;
+                }
+                ids = g;
+            }
+            ids[cnt++] = x;
+        }
+        i = j + 1;
+    }
+    if (bad) {
+        free(ids);
+        return -1;
+    }
+    qsort(ids, cnt, sizeof *ids, cmp_i64);
+    int64_t distinct = 0;
+    for (size_t q = 0; q < cnt; q++) distinct += q == 0 || ids[q] != ids[q - 1];
+    free(ids);
+    *tasks = distinct;
+    *running = (limit > 0 && limit < distinct) ? limit : distinct;
+    return 0;
+}
+
+/* One sizecar pod's admission requests: the script's #SBATCH header
+ * (extractBatchResourcesFromScript, parse.go:30-69) under the labels newSubmitRequestForPod
+ * reads (provider.go:74-123: strconv.ParseInt, skipped on error), which getSbatchOpts passes as
+ * command-line flags that win over #SBATCH lines (pkg/slurm-agent/slurm.go:189-229); defaults
+ * pod.go:97-107; ref_job_demand; one request per simultaneously running array task.
+ * labels[6] = nodes, cpus-per-task, mem-per-cpu, ntasks-per-node, array, ntask (NULL = absent).
+ * out[i*4 + 0..3] = cpu, mem, wall, k for min(n, cap) tasks.  Returns n, or -1 (malformed header
+ * or array, the reference's error / panic cases included) / -2 (demand out of range). */
+int ref_pod_demand(const char* const* labels, const char* script, int32_t* out, int cap) {
+    ref_job_resources r;
+    memset(&r, 0, sizeof r);
+    if (script && ref_extract_batch_resources(script, &r) != 0) return -1;
+    int64_t v[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 6; i++) {
+        if (i == 4 || !labels[i]) continue;
+        int64_t x;
+        if (go_parse_int(labels[i], strlen(labels[i]), &x) == 0) v[i] = x;
+    }
+    ref_apply_spec_and_defaults(&r, v[0], v[1], v[2], v[3], NULL, v[5]);
+    int32_t c, m, w;
+    uint16_t k;
+    if (ref_job_demand(&r, &c, &m, &w, &k) != 0 || k > 8) return -2;
+    int64_t tasks = 1, running = 1;
+    if (labels[4] && labels[4][0] && ref_array_tasks(labels[4], &tasks, &running) != 0) return -1;
+    for (int64_t i = 0; i < running && i < cap; i++) {
+        out[i * 4 + 0] = c;
+        out[i * 4 + 1] = m;
+        out[i * 4 + 2] = w;
+        out[i * 4 + 3] = k;
+    }
+    return (int)running;
+}
+
 /* GetPartitionCapacity pkg/slurm-virtual-kubelet/node.go:169-199 */
 void ref_partition_capacity(const ref_node* nodes, int n, int64_t* cpu, int64_t* memory,
                             int64_t* gpu, int64_t* pods) {

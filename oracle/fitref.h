@@ -59,6 +59,11 @@ void ref_apply_spec_and_defaults(ref_job_resources* r, int64_t nodes, int64_t cp
 int64_t ref_parse_array_len(const char* array);
 /* genResourceListForPod (pod.go:143-162): cpu count and memory quantity (bytes, as the ref). */
 void ref_pod_request(const ref_job_resources* r, int64_t* cpu, int64_t* memory);
+/* DESIGN.md §2 per-node demand; Slurm --array task count; a pod's admission requests. */
+int ref_job_demand(const ref_job_resources* r, int32_t* cpu, int32_t* mem, int32_t* wall,
+                   uint16_t* k);
+int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running);
+int ref_pod_demand(const char* const* labels, const char* script, int32_t* out, int cap);
 /* GetPartitionCapacity (pkg/slurm-virtual-kubelet/node.go:169-199). */
 void ref_partition_capacity(const ref_node* nodes, int n, int64_t* cpu, int64_t* memory,
                             int64_t* gpu, int64_t* pods);

@@ -10,7 +10,9 @@ namespace fitgpu {
 constexpr int KS = FIT_KS;      // candidates kept per (job, block-slice) by fit_scan
 // the per-wave insertion network and the LDS bitonic merge tree of k_scan need a power of two
 // (a FIT_KS=12 build placed jobs wrongly before this check)
-static_assert(KS >= 2 && KS <= 64 && (KS & (KS - 1)) == 0, "FIT_KS must be a power of two in [2, 64]");
+// k_engine's workers dispatch on the per-component key count with cases 16, 8, 4 and 2 only
+// (fit_persistent.hip): a larger FIT_KS would have no case
+static_assert(KS >= 2 && KS <= 16 && (KS & (KS - 1)) == 0, "FIT_KS must be a power of two in [2, 16]");
 constexpr int SCAN_WAVES = 8;   // waves per scan block; each walks one sub-slice of nodes
 constexpr int SCAN_JOBS = 64;   // jobs per scan block (lanes = jobs, shared by the 8 waves)
 #ifndef FIT_MIN_SUB

@@ -242,9 +242,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 SCAN_K(16)
                 SCAN_K(8)
                 SCAN_K(4)
-                default:
                 SCAN_K(2)
 #undef SCAN_K
+                default:  // no scan kernel for this key count: trip the watchdog, never guess
+                    if (threadIdx.x == 0) atomicOr(&ctl->error, 8u);
+                    break;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
 #ifdef FIT_STAMPS

@@ -362,7 +362,7 @@ int fit_job_demand(const fit_job_resources* r, int32_t* cpu, int32_t* mem_mib, i
     const int64_t k = r->nodes > 0 ? r->nodes : 1;
     int64_t tpn = 1;
     if (r->ntasks_per_node > 0) tpn = r->ntasks_per_node;
-    else if (r->ntasks > 0) tpn = (r->ntasks + k - 1) / k;
+    else if (r->ntasks > 0) tpn = r->ntasks / k + (r->ntasks % k != 0);  // no overflow at INT64_MAX
     const int64_t cpt = r->cpus_per_task > 0 ? r->cpus_per_task : 1;
     const int64_t mpc = r->mem_per_cpu > 0 ? r->mem_per_cpu : 1024;
     if (k > 65535 || tpn > INT32_MAX || cpt > INT32_MAX || tpn * cpt > INT32_MAX ||
@@ -584,6 +584,178 @@ int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32
     if (names) {
         const int rc = put_names(node_names, names, names_len);
         if (rc < 0) return rc;
+    }
+    return n;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------- CreatePod call site (a10)
+// What CreatePod (pkg/slurm-virtual-kubelet/provider.go:35-60) holds — the pod's labels and its
+// script — turned into engine requests, and the engine's decision written back into the script
+// (include/fitgpu.h "CreatePod call site").  The Go side passes strings through; every rule
+// lives here, where the tests reach it.
+
+namespace {
+
+// Slurm --array item "a", "a-b" or "a-b:s" → its ids into `ids` (a bitmap over task ids)
+bool array_item(sv it, std::vector<bool>& ids) {
+    constexpr int64_t MAX_ID = (1 << 22) - 1;
+    sv range = it, step;
+    const size_t colon = it.find(':');
+    if (colon != sv::npos) {
+        range = it.substr(0, colon);
+        step = it.substr(colon + 1);
+    }
+    const size_t dash = range.find('-');
+    sv lo = dash == sv::npos ? range : range.substr(0, dash);
+    sv hi = dash == sv::npos ? range : range.substr(dash + 1);
+    int64_t a, b, s = 1;
+    auto digits = [](sv x) { return !x.empty() && x.find_first_not_of("0123456789") == sv::npos; };
+    if (!digits(lo) || !digits(hi) || parse_int(lo, a) || parse_int(hi, b) || b < a || b > MAX_ID)
+        return false;
+    if (colon != sv::npos && (dash == sv::npos || !digits(step) || parse_int(step, s) || s < 1))
+        return false;
+    if ((int64_t)ids.size() <= b) ids.resize((size_t)b + 1, false);
+    for (int64_t x = a; x <= b; x += s) ids[(size_t)x] = true;
+    return true;
+}
+
+// a label value as newSubmitRequestForPod reads it: strconv.ParseInt(v, 10, 64), skipped on error
+int64_t label_int(const char* v) {
+    if (!v) return 0;
+    int64_t x;
+    return parse_int(sv(v), x) == 0 ? x : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running) {
+    if (!array || !tasks || !max_running) return FIT_E_INVAL;
+    sv a = trim_space(sv(array));
+    int64_t limit = INT64_MAX;
+    const size_t pct = a.find('%');
+    if (pct != sv::npos) {
+        const sv l = a.substr(pct + 1);
+        if (l.empty() || l.find_first_not_of("0123456789") != sv::npos || parse_int(l, limit) ||
+            limit < 1)
+            return FIT_E_PARSE;
+        a = a.substr(0, pct);
+    }
+    if (a.empty()) return FIT_E_PARSE;
+    std::vector<bool> ids;
+    for (sv it : split(a, ","))
+        if (!array_item(it, ids)) return FIT_E_PARSE;
+    int64_t n = 0;
+    for (bool b : ids) n += b;
+    *tasks = n;
+    *max_running = n < limit ? n : limit;
+    return FIT_OK;
+}
+
+int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
+                   int64_t priority, fit_admit_req* out, int32_t cap) {
+    if (cap < 0 || (cap > 0 && !out)) return FIT_E_INVAL;
+    fit_pod_labels none{};
+    const fit_pod_labels& L = labels ? *labels : none;
+    fit_job_resources r{};
+    if (script) {
+        const int rc = fit_extract_batch_resources(script, &r);  // parse.go:30-69
+        if (rc) return rc;
+    }
+    // the labels reach sbatch as command-line flags, which override the #SBATCH lines; the array
+    // is counted from the full label (fit_apply_spec keeps 63 characters of it)
+    fit_apply_spec(&r, label_int(L.nodes), label_int(L.cpus_per_task), label_int(L.mem_per_cpu),
+                   label_int(L.ntasks_per_node), nullptr, label_int(L.ntasks));
+    int32_t cpu, mem, wall;
+    uint16_t k;
+    const int rc = fit_job_demand(&r, &cpu, &mem, &wall, &k);
+    if (rc) return rc;
+    if (k > FIT_MAX_K) return FIT_E_INVAL;
+    int64_t tasks = 1, running = 1;
+    if (L.array && L.array[0]) {
+        const int ra = fit_array_tasks(L.array, &tasks, &running);
+        if (ra) return ra;
+    }
+    if (running > INT32_MAX) return FIT_E_INVAL;
+    for (int64_t i = 0; i < running && i < cap; ++i)
+        out[i] = fit_admit_req{priority, cpu, mem, 0, wall, part, k};
+    return (int)running;
+}
+
+int fit_script_with_nodelist(const char* script, const char* names, int32_t n_names,
+                             const int32_t* node, int32_t k, char* out, int32_t outlen) {
+    if (!script || (n_names > 0 && !names) || n_names < 0 || k < 1 || k > FIT_MAX_K || !node ||
+        !out || outlen < 1)
+        return FIT_E_INVAL;
+    std::vector<sv> nm;
+    nm.reserve((size_t)n_names);
+    for (const char* p = names; (int32_t)nm.size() < n_names; p += strlen(p) + 1) nm.push_back(p);
+    std::string dir = "#SBATCH --nodelist=";
+    for (int32_t i = 0; i < k; ++i) {
+        if (node[i] < 0 || node[i] >= n_names || nm[(size_t)node[i]].empty()) return FIT_E_INVAL;
+        if (i) dir += ',';
+        dir.append(nm[(size_t)node[i]]);
+    }
+    dir += '\n';
+    // the header: the leading lines extractBatchResourcesFromScript walks (parse.go:36-52) —
+    // empty lines, "#!" lines and "#SBATCH" lines; the directive goes after its last #SBATCH
+    // line (or the shebang / nothing when there is none)
+    const sv s(script);
+    size_t pos = 0, ins = 0;
+    bool seen_sbatch = false;
+    while (pos < s.size()) {
+        const size_t nl = s.find('\n', pos);
+        const size_t end = nl == sv::npos ? s.size() : nl + 1;
+        sv line = s.substr(pos, (nl == sv::npos ? s.size() : nl) - pos);
+        if (!line.empty() && line.back() == '\r') line.remove_suffix(1);
+        if (line.substr(0, 7) == "#SBATCH") {
+            seen_sbatch = true;
+            ins = end;
+        } else if (line.empty() || line.substr(0, 2) == "#!") {
+            if (!seen_sbatch && line.substr(0, 2) == "#!") ins = end;
+        } else {
+            break;
+        }
+        pos = end;
+    }
+    std::string res;
+    res.reserve(s.size() + dir.size() + 1);
+    res.append(s.substr(0, ins));
+    if (ins > 0 && s[ins - 1] != '\n') res += '\n';  // a header that ends without a newline
+    res += dir;
+    res.append(s.substr(ins));
+    if ((int64_t)res.size() + 1 > outlen) return FIT_E_INVAL;
+    memcpy(out, res.data(), res.size());
+    out[res.size()] = 0;
+    return (int)res.size();
+}
+
+int fit_partition_limits(int64_t wall_time_s, int64_t cpu_per_node, int64_t mem_per_node,
+                         int32_t* max_time_min, int32_t* max_cpus_per_node,
+                         int32_t* max_mem_per_node) {
+    if (!max_time_min || !max_cpus_per_node || !max_mem_per_node) return FIT_E_INVAL;
+    // ≤ 0: UNLIMITED (parseResources' -1, parse.go:128-187; a -1 ns walltime is 0 s after
+    // api/slurm.go:309) or unset (0)
+    auto lim = [](int64_t v) { return v <= 0 ? -1 : v > INT32_MAX ? INT32_MAX : (int32_t)v; };
+    *max_time_min = wall_time_s <= 0 ? -1 : lim((wall_time_s + 59) / 60);
+    *max_cpus_per_node = lim(cpu_per_node);
+    *max_mem_per_node = lim(mem_per_node);
+    return FIT_OK;
+}
+
+int fit_node_columns(const fit_node* nodes, int32_t n, uint32_t part_mask, int32_t* cpu_free,
+                     int32_t* mem_free, int32_t* gpu_free, int32_t* avail_min, uint32_t* mask) {
+    if (n < 0 || (n > 0 && (!nodes || !cpu_free || !mem_free || !gpu_free || !avail_min || !mask)))
+        return FIT_E_INVAL;
+    for (int32_t i = 0; i < n; ++i) {  // free = total − alloc (workload.proto:165-174)
+        cpu_free[i] = to_i32(nodes[i].cpus - nodes[i].allo_cpus);
+        mem_free[i] = to_i32(nodes[i].memory - nodes[i].allo_memory);
+        gpu_free[i] = to_i32(nodes[i].gpus - nodes[i].allo_gpus);
+        avail_min[i] = INT32_MAX;
+        mask[i] = part_mask;
     }
     return n;
 }

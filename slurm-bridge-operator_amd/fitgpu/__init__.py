@@ -20,14 +20,16 @@ Every compute call goes through the HIP library; nothing here computes a placeme
 from __future__ import annotations
 
 import ctypes as C
+import threading
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (FIT_E_PARSE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO, FIT_SHARD_COMPONENTS,
-                   FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32,
-                   FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError, FitJobResources, FitNode,
-                   FitOpts, FitResources, FitStats, check, lib)
+from ._lib import (FIT_E_PARSE, FIT_E_STATE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO,
+                   FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32,
+                   FIT_XCHG_MIN_I32, FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError, FitJobResources,
+                   FitNode, FitOpts, FitPodLabels, FitResources, FitStats, check, lib)
 
 __all__ = [
     "Engine", "FitError", "ErrDurationIsUnlimited", "ParseDuration", "parse_resources", "parse_nodes",
@@ -35,7 +37,8 @@ __all__ = [
     "parse_array_len", "gen_resource_list_for_pod", "job_demand", "get_partition_capacity",
     "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
     "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS", "expand_hostlist", "ingest_nodes",
-    "FIT_FLAG_COLLECTIVES", "Admitter",
+    "FIT_FLAG_COLLECTIVES", "Admitter", "array_tasks", "pod_demand", "script_with_nodelist",
+    "partition_limits", "node_columns", "POD_LABEL_KEYS",
 ]
 
 
@@ -213,6 +216,73 @@ def get_partition_capacity(nodes: list[Node]) -> dict:
     return out
 
 
+# ---------------------------------------------------------------- CreatePod call site
+# pkg/common/labels.go:9-14, the keys newSubmitRequestForPod reads (provider.go:74-123)
+POD_LABEL_KEYS = {"nodes": "sbo.kubecluster.org/nodes", "cpus_per_task": "sbo.kubecluster.org/cpus-per-task",
+                  "mem_per_cpu": "sbo.kubecluster.org/mem-per-cpu",
+                  "ntasks_per_node": "sbo.kubecluster.org/ntasks-per-node",
+                  "array": "sbo.kubecluster.org/array", "ntasks": "sbo.kubecluster.org/ntask"}
+
+
+def array_tasks(array: str) -> tuple[int, int]:
+    """(distinct task ids, tasks that may run at once) of a Slurm --array expression."""
+    n, r = C.c_int64(), C.c_int64()
+    rc = lib().fit_array_tasks(array.encode(), C.byref(n), C.byref(r))
+    if rc == FIT_E_PARSE:
+        raise ValueError(f"malformed array {array!r}")
+    check(rc, "fit_array_tasks")
+    return n.value, r.value
+
+
+def pod_demand(labels: dict, script: str | None, part: int = 0, priority: int = 0) -> list[tuple]:
+    """A pod's admission requests from its labels (keys of POD_LABEL_KEYS' values) and script:
+    [(priority, cpu, mem_mib, gpu, wall_min, part, nodes_k)] — one per array task that may run
+    at once (include/fitgpu.h fit_pod_demand)."""
+    byname = {v: k for k, v in POD_LABEL_KEYS.items()}
+    vals = {byname[k]: str(v).encode() for k, v in labels.items() if k in byname}
+    lab = FitPodLabels(*(vals.get(k) for k in ("nodes", "cpus_per_task", "mem_per_cpu", "ntasks_per_node",
+                                               "array", "ntasks")))
+    scr = script.encode() if script is not None else None
+    n = lib().fit_pod_demand(C.byref(lab), scr, part, priority, None, 0)
+    if n == FIT_E_PARSE:
+        raise ValueError("malformed #SBATCH header or array expression")
+    check(n, "fit_pod_demand")
+    out = (FitAdmitReq * n)()
+    check(lib().fit_pod_demand(C.byref(lab), scr, part, priority, out, n), "fit_pod_demand")
+    return [(r.priority, r.cpu, r.mem_mib, r.gpu, r.wall_min, r.part, r.nodes_k) for r in out]
+
+
+def script_with_nodelist(script: str, names: list[str], nodes: list[int]) -> str:
+    """The script with `#SBATCH --nodelist=` for the engine's nodes (fit_script_with_nodelist)."""
+    blob = b"".join(x.encode() + b"\0" for x in names)
+    outlen = len(script.encode()) + 32 + len(blob) + 1
+    buf = C.create_string_buffer(outlen)
+    ids = (C.c_int32 * len(nodes))(*nodes)
+    n = check(lib().fit_script_with_nodelist(script.encode(), blob, len(names), ids, len(nodes), buf, outlen),
+              "fit_script_with_nodelist")
+    return buf.raw[:n].decode()
+
+
+def partition_limits(wall_time_s: int, cpu_per_node: int, mem_per_node: int) -> tuple[int, int, int]:
+    """ResourcesResponse fields → (max_time_min, max_cpus_per_node, max_mem_per_node), -1 = none."""
+    a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+    check(lib().fit_partition_limits(wall_time_s, cpu_per_node, mem_per_node, C.byref(a), C.byref(b), C.byref(c)),
+          "fit_partition_limits")
+    return a.value, b.value, c.value
+
+
+def node_columns(nodes: list[Node], part_mask: int = 1):
+    """NodesResponse rows → synth.Nodes columns (free = total − alloc) for load_nodes."""
+    from .synth import Nodes
+    n = len(nodes)
+    arr = (FitNode * max(n, 1))()
+    for i, x in enumerate(nodes):
+        arr[i] = FitNode(x.Cpus, x.Memory, x.Gpus, x.AlloCpus, x.AlloMemory, x.AlloGpus)
+    cols = [np.empty(max(n, 1), np.int32) for _ in range(4)] + [np.empty(max(n, 1), np.uint32)]
+    check(lib().fit_node_columns(arr, n, part_mask, *[_ptr(c) for c in cols]), "fit_node_columns")
+    return Nodes(*(c[:n].copy() for c in cols))
+
+
 # ------------------------------------------------------------------------------- engine
 def nccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
@@ -271,8 +341,11 @@ class Engine:
         check(lib().fit_create(C.byref(o), C.byref(h)), "fit_create")
         self._h = h
         self.n = 0
+        self._admitters = weakref.WeakSet()  # closed before the context goes (Admitter holds it)
 
     def close(self):
+        for a in list(getattr(self, "_admitters", ())):
+            a.close()
         if getattr(self, "_h", None):
             lib().fit_destroy(self._h)
             self._h = None
@@ -388,42 +461,102 @@ class Admitter:
     """Batched admission over one Engine (include/fitgpu.h "batched admission"; the CreatePod
     call site of pkg/slurm-virtual-kubelet/provider.go:35-60).  `admit` blocks the calling thread
     until its batch is placed (ctypes releases the GIL, so threads admit concurrently, as the 10
-    PodSyncWorkers do) and returns (nodes, batch, batch_jobs, order); nodes[0] is FIT_UNPLACED /
-    FIT_REJECTED when the pod cannot be placed now."""
+    PodSyncWorkers do) and returns (nodes, batch, batch_jobs, order, ticket); nodes[0] is
+    FIT_UNPLACED / FIT_REJECTED when the pod cannot be placed now.
+
+    Lifetime: close() (also Engine.close()) stops new calls, waits for the calls already inside
+    (their batches are still placed), then destroys the native admitter — a caller can never hold
+    a handle that is being freed."""
 
     def __init__(self, engine: Engine, max_batch: int = 1024, max_wait_us: int = 2000):
         self._engine = engine  # keeps the context alive
         h = C.c_void_p()
         check(lib().fit_admitter_create(engine._h, max_batch, max_wait_us, C.byref(h)), "fit_admitter_create")
         self._h = h
+        self._cv = threading.Condition()
+        self._users = 0
+        engine._admitters.add(self)
+
+    def _enter(self):
+        with self._cv:
+            if not self._h:
+                raise FitError(FIT_E_STATE, "Admitter closed")
+            self._users += 1
+            return self._h
+
+    def _leave(self):
+        with self._cv:
+            self._users -= 1
+            self._cv.notify_all()
+
+    def _call(self, fn, *args):
+        h = self._enter()
+        try:
+            return fn(h, *args)
+        finally:
+            self._leave()
+
+    @staticmethod
+    def _res(r, nodes_k):
+        k = max(nodes_k, 1)
+        nodes = [r.node[i] for i in range(k)] if r.node[0] >= 0 else [r.node[0]]
+        return nodes, r.batch, r.batch_jobs, r.order, r.ticket
 
     def admit(self, priority: int, cpu: int, mem_mib: int, gpu: int = 0, wall_min: int = 0,
               part: int = 0, nodes_k: int = 1):
         q = FitAdmitReq(priority, cpu, mem_mib, gpu, wall_min, part, nodes_k)
         r = FitAdmitRes()
-        check(lib().fit_admit(self._h, C.byref(q), C.byref(r)), "fit_admit")
-        k = max(nodes_k, 1)
-        nodes = [r.node[i] for i in range(k)] if r.node[0] >= 0 else [r.node[0]]
-        return nodes, r.batch, r.batch_jobs, r.order
+        check(self._call(lambda h: lib().fit_admit(h, C.byref(q), C.byref(r))), "fit_admit")
+        return self._res(r, nodes_k)
+
+    def admit_group(self, reqs: list[tuple]):
+        """All-or-nothing admission of (priority, cpu, mem, gpu, wall, part, k) requests (the
+        tasks of one array job, pod_demand's output); one result per request."""
+        n = len(reqs)
+        q = (FitAdmitReq * n)(*[FitAdmitReq(*r) for r in reqs])
+        r = (FitAdmitRes * n)()
+        check(self._call(lambda h: lib().fit_admit_group(h, q, n, r)), "fit_admit_group")
+        return [self._res(r[i], reqs[i][6]) for i in range(n)]
 
     def load_nodes(self, nodes):
         cols = [np.ascontiguousarray(nodes.cpu_free, np.int32), np.ascontiguousarray(nodes.mem_free, np.int32),
                 np.ascontiguousarray(nodes.gpu_free, np.int32), np.ascontiguousarray(nodes.avail_min, np.int32),
                 np.ascontiguousarray(nodes.part_mask, np.uint32)]
-        check(lib().fit_admitter_load_nodes(self._h, len(cols[0]), *[_ptr(c) for c in cols]),
+        check(self._call(lambda h: lib().fit_admitter_load_nodes(h, len(cols[0]), *[_ptr(c) for c in cols])),
               "fit_admitter_load_nodes")
         self._engine.n = len(cols[0])
 
     def partition_free(self, p: int):
         c, m, g = C.c_int64(), C.c_int64(), C.c_int64()
-        check(lib().fit_admitter_partition_free(self._h, p, C.byref(c), C.byref(m), C.byref(g)),
+        check(self._call(lambda h: lib().fit_admitter_partition_free(h, p, C.byref(c), C.byref(m), C.byref(g))),
               "fit_admitter_partition_free")
         return {"cpu": c.value, "mem_mib": m.value, "gpu": g.value}
 
+    def confirm(self, ticket: int):
+        check(self._call(lambda h: lib().fit_admitter_confirm(h, ticket)), "fit_admitter_confirm")
+
+    def release(self, ticket: int):
+        check(self._call(lambda h: lib().fit_admitter_release(h, ticket)), "fit_admitter_release")
+
+    def set_ttl(self, loads: int):
+        check(self._call(lambda h: lib().fit_admitter_set_ttl(h, loads)), "fit_admitter_set_ttl")
+
+    def reservations(self) -> int:
+        return check(self._call(lambda h: lib().fit_admitter_reservations(h)), "fit_admitter_reservations")
+
+    def pending(self) -> int:
+        return check(self._call(lambda h: lib().fit_admitter_pending(h)), "fit_admitter_pending")
+
     def close(self):
-        if getattr(self, "_h", None):
-            lib().fit_admitter_destroy(self._h)
-            self._h = None
+        cv = getattr(self, "_cv", None)
+        if cv is None:
+            return
+        with cv:
+            h, self._h = self._h, None  # no new calls
+            while self._users:
+                cv.wait()  # calls already inside finish (their batches are placed)
+        if h:
+            lib().fit_admitter_destroy(h)
 
     def __del__(self):
         self.close()
@@ -433,4 +566,3 @@ class Admitter:
 
     def __exit__(self, *a):
         self.close()
-

@@ -34,8 +34,11 @@ EXPORTS = [
     "fit_pod_request", "fit_job_demand", "fit_partition_capacity",
     "fit_load_timeline", "fit_load_timeline_device", "fit_place_tl", "fit_place_tl_device",
     "fit_read_timeline", "fit_ingest_nodes", "fit_expand_hostlist",
-    "fit_admitter_create", "fit_admit", "fit_admitter_load_nodes", "fit_admitter_partition_free",
-    "fit_admitter_destroy",
+    "fit_admitter_create", "fit_admit", "fit_admit_group", "fit_admitter_load_nodes",
+    "fit_admitter_partition_free", "fit_admitter_confirm", "fit_admitter_release", "fit_admitter_set_ttl",
+    "fit_admitter_reservations", "fit_admitter_pending", "fit_admitter_destroy",
+    "fit_array_tasks", "fit_pod_demand", "fit_script_with_nodelist", "fit_partition_limits",
+    "fit_node_columns",
 ]
 
 
@@ -76,7 +79,12 @@ class FitAdmitReq(C.Structure):
 
 class FitAdmitRes(C.Structure):
     _fields_ = [("node", C.c_int32 * FIT_MAX_K), ("batch", C.c_int64), ("batch_jobs", C.c_int32),
-                ("order", C.c_int32)]
+                ("order", C.c_int32), ("ticket", C.c_int64)]
+
+
+class FitPodLabels(C.Structure):
+    _fields_ = [(n, C.c_char_p) for n in ("nodes", "cpus_per_task", "mem_per_cpu", "ntasks_per_node", "array",
+                                          "ntasks")]
 
 
 class FitResources(C.Structure):
@@ -133,8 +141,20 @@ def lib() -> C.CDLL:
         L.fit_admitter_load_nodes.argtypes = [P, i32, P, P, P, P, P]
         L.fit_admitter_partition_free.argtypes = [P, i32, C.POINTER(i64), C.POINTER(i64),
                                                   C.POINTER(i64)]
+        L.fit_admit_group.argtypes = [P, C.POINTER(FitAdmitReq), i32, C.POINTER(FitAdmitRes)]
+        for name in ("fit_admitter_confirm", "fit_admitter_release"):
+            getattr(L, name).argtypes = [P, i64]
+        L.fit_admitter_set_ttl.argtypes = [P, i32]
+        L.fit_admitter_reservations.argtypes = [P]
+        L.fit_admitter_pending.argtypes = [P]
         L.fit_admitter_destroy.argtypes = [P]
         L.fit_admitter_destroy.restype = None
+        L.fit_array_tasks.argtypes = [C.c_char_p, C.POINTER(i64), C.POINTER(i64)]
+        L.fit_pod_demand.argtypes = [C.POINTER(FitPodLabels), C.c_char_p, C.c_uint16, i64, C.POINTER(FitAdmitReq),
+                                     i32]
+        L.fit_script_with_nodelist.argtypes = [C.c_char_p, C.c_char_p, i32, C.POINTER(i32), i32, C.c_char_p, i32]
+        L.fit_partition_limits.argtypes = [i64, i64, i64, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+        L.fit_node_columns.argtypes = [C.POINTER(FitNode), i32, C.c_uint32, P, P, P, P, P]
         L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]
         L.fit_parse_nodes.argtypes = [C.c_char_p, C.POINTER(FitNode), i32]

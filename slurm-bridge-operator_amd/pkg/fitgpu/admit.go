@@ -21,7 +21,7 @@ type Admitter struct {
 	eng *Engine // keeps the context alive
 }
 
-// Demand of one pod (per node), as fit_job_demand derives it from the SlurmBridgeJob labels.
+// Demand of one pod (per node), as fit_pod_demand derives it (PodDemand).
 type Demand struct {
 	Priority int64 // smaller first: e.g. pod.CreationTimestamp.UnixNano()
 	CPU      int32
@@ -32,15 +32,16 @@ type Demand struct {
 	NodesK   uint16 // --nodes (0 = 1, <= MaxK)
 }
 
-// Admission is the engine's answer for one pod.
+// Admission is the engine's answer for one request.
 type Admission struct {
 	Nodes     []int32 // node ids (NodesK of them), or [Unplaced] / [Rejected]
-	Batch     int64   // batch the pod was placed in
-	BatchJobs int32   // pods placed together in that batch
-	Order     int32   // this pod's position in the batch's placement order
+	Batch     int64   // batch the request was placed in
+	BatchJobs int32   // requests placed together in that batch
+	Order     int32   // this request's position in the batch's placement order
+	Ticket    int64   // reservation (> 0 when placed): Confirm once Slurm runs it, Release if not
 }
 
-// Placed reports whether the pod got its nodes.
+// Placed reports whether the request got its nodes.
 func (a Admission) Placed() bool { return len(a.Nodes) > 0 && a.Nodes[0] >= 0 }
 
 // NewAdmitter starts the coalescer: a batch closes maxWait after its first request or at
@@ -50,7 +51,9 @@ func NewAdmitter(e *Engine, maxBatch int, maxWait time.Duration) (*Admitter, err
 		return nil, fmt.Errorf("fitgpu: NewAdmitter on a closed engine")
 	}
 	var a *C.fit_admitter
-	if err := check(C.fit_admitter_create(e.ctx, C.int32_t(maxBatch), C.int32_t(maxWait.Microseconds()), &a)); err != nil {
+	rc := C.fit_admitter_create(e.ctx, C.int32_t(maxBatch), C.int32_t(maxWait.Microseconds()), &a)
+	runtime.KeepAlive(e)
+	if err := check(rc); err != nil {
 		return nil, err
 	}
 	ad := &Admitter{a: a, eng: e}
@@ -58,25 +61,21 @@ func NewAdmitter(e *Engine, maxBatch int, maxWait time.Duration) (*Admitter, err
 	return ad, nil
 }
 
-// Admit blocks until the pod's batch is placed.
-func (ad *Admitter) Admit(d Demand) (Admission, error) {
-	if d.NodesK > MaxK {
-		return Admission{}, fmt.Errorf("fitgpu: nodes %d > %d", d.NodesK, MaxK)
-	}
-	req := C.fit_admit_req{
+func cReq(d Demand) C.fit_admit_req {
+	return C.fit_admit_req{
 		priority: C.int64_t(d.Priority), cpu: C.int32_t(d.CPU), mem_mib: C.int32_t(d.MemMiB),
 		gpu: C.int32_t(d.GPU), wall_min: C.int32_t(d.WallMin), part: C.uint16_t(d.Part),
 		nodes_k: C.uint16_t(d.NodesK),
 	}
-	var res C.fit_admit_res
-	if err := check(C.fit_admit(ad.a, &req, &res)); err != nil {
-		return Admission{}, err
-	}
-	k := int(d.NodesK)
+}
+
+func goRes(res *C.fit_admit_res, nodesK uint16) Admission {
+	k := int(nodesK)
 	if k < 1 {
 		k = 1
 	}
-	out := Admission{Batch: int64(res.batch), BatchJobs: int32(res.batch_jobs), Order: int32(res.order)}
+	out := Admission{Batch: int64(res.batch), BatchJobs: int32(res.batch_jobs), Order: int32(res.order),
+		Ticket: int64(res.ticket)}
 	if res.node[0] < 0 {
 		out.Nodes = []int32{int32(res.node[0])}
 	} else {
@@ -85,28 +84,95 @@ func (ad *Admitter) Admit(d Demand) (Admission, error) {
 			out.Nodes[i] = int32(res.node[i])
 		}
 	}
+	return out
+}
+
+// Admit blocks until the request's batch is placed.
+func (ad *Admitter) Admit(d Demand) (Admission, error) {
+	if d.NodesK > MaxK {
+		return Admission{}, fmt.Errorf("fitgpu: nodes %d > %d", d.NodesK, MaxK)
+	}
+	req := cReq(d)
+	var res C.fit_admit_res
+	rc := C.fit_admit(ad.a, &req, &res)
+	runtime.KeepAlive(ad) // the finalizer must not destroy the admitter during the blocking call
+	if err := check(rc); err != nil {
+		return Admission{}, err
+	}
+	return goRes(&res, d.NodesK), nil
+}
+
+// AdmitGroup admits the requests of one pod (PodDemand's tasks) all or nothing, in one batch.
+func (ad *Admitter) AdmitGroup(ds []Demand) ([]Admission, error) {
+	if len(ds) == 0 {
+		return nil, nil
+	}
+	reqs := make([]C.fit_admit_req, len(ds))
+	for i, d := range ds {
+		if d.NodesK > MaxK {
+			return nil, fmt.Errorf("fitgpu: nodes %d > %d", d.NodesK, MaxK)
+		}
+		reqs[i] = cReq(d)
+	}
+	res := make([]C.fit_admit_res, len(ds))
+	rc := C.fit_admit_group(ad.a, &reqs[0], C.int32_t(len(ds)), &res[0])
+	runtime.KeepAlive(ad)
+	if err := check(rc); err != nil {
+		return nil, err
+	}
+	out := make([]Admission, len(ds))
+	for i := range ds {
+		out[i] = goRes(&res[i], ds[i].NodesK)
+	}
 	return out, nil
 }
 
-// LoadNodes replaces the node table between batches (the node refresh ticker).
+// LoadNodes replaces the node table between batches (the node refresh ticker); open reservations
+// are taken from the new table again.
 func (ad *Admitter) LoadNodes(n Nodes) error {
 	cnt := len(n.CPUFree)
 	if !sameLen(cnt, len(n.MemFreeMiB), len(n.GPUFree), len(n.AvailMin), len(n.PartMask)) {
 		return errLen
 	}
+	var rc C.int
 	if cnt == 0 {
-		return check(C.fit_admitter_load_nodes(ad.a, 0, nil, nil, nil, nil, nil))
+		rc = C.fit_admitter_load_nodes(ad.a, 0, nil, nil, nil, nil, nil)
+	} else {
+		rc = C.fit_admitter_load_nodes(ad.a, C.int32_t(cnt),
+			(*C.int32_t)(&n.CPUFree[0]), (*C.int32_t)(&n.MemFreeMiB[0]), (*C.int32_t)(&n.GPUFree[0]),
+			(*C.int32_t)(&n.AvailMin[0]), (*C.uint32_t)(&n.PartMask[0]))
 	}
-	return check(C.fit_admitter_load_nodes(ad.a, C.int32_t(cnt),
-		(*C.int32_t)(&n.CPUFree[0]), (*C.int32_t)(&n.MemFreeMiB[0]), (*C.int32_t)(&n.GPUFree[0]),
-		(*C.int32_t)(&n.AvailMin[0]), (*C.uint32_t)(&n.PartMask[0])))
+	runtime.KeepAlive(ad)
+	return check(rc)
 }
 
 // PartitionFree is the allocation-aware free capacity of partition p after the admitted pods.
 func (ad *Admitter) PartitionFree(p int) (cpu, memMiB, gpu int64, err error) {
 	var c, m, g C.int64_t
 	err = check(C.fit_admitter_partition_free(ad.a, C.int32_t(p), &c, &m, &g))
+	runtime.KeepAlive(ad)
 	return int64(c), int64(m), int64(g), err
+}
+
+// Confirm: Slurm now counts the job (it is allocated); the reservation ends at the next LoadNodes.
+func (ad *Admitter) Confirm(ticket int64) error {
+	err := check(C.fit_admitter_confirm(ad.a, C.int64_t(ticket)))
+	runtime.KeepAlive(ad)
+	return err
+}
+
+// Release: the job will not run (pod deleted, SubmitJob failed); its demand goes back now.
+func (ad *Admitter) Release(ticket int64) error {
+	err := check(C.fit_admitter_release(ad.a, C.int64_t(ticket)))
+	runtime.KeepAlive(ad)
+	return err
+}
+
+// SetTTL drops an open reservation after `loads` node-table loads (0 = never).
+func (ad *Admitter) SetTTL(loads int) error {
+	err := check(C.fit_admitter_set_ttl(ad.a, C.int32_t(loads)))
+	runtime.KeepAlive(ad)
+	return err
 }
 
 // Close stops the coalescer; still-queued Admit calls return FIT_E_STATE.
@@ -115,23 +181,4 @@ func (ad *Admitter) Close() {
 		C.fit_admitter_destroy(ad.a)
 		ad.a = nil
 	}
-}
-
-// DemandFromLabels derives a pod's per-node demand from the sbo.kubecluster.org/* labels that
-// newSubmitRequestForPod reads (pkg/slurm-virtual-kubelet/provider.go:62-125,
-// pkg/common/labels.go:9-14) through the engine's mirror of the operator's arithmetic
-// (fit_apply_spec + fit_job_demand, pkg/slurm-bridge-operator/pod.go:70-162).  Missing labels
-// are 0 (the operator's defaults then apply); wallMin comes from the job's --time.
-func DemandFromLabels(nodes, cpusPerTask, memPerCPU, nTasksPerNode, nTasks int64, wallMin int32,
-	part uint16, priority int64) (Demand, error) {
-	var r C.fit_job_resources
-	C.fit_apply_spec(&r, C.int64_t(nodes), C.int64_t(cpusPerTask), C.int64_t(memPerCPU),
-		C.int64_t(nTasksPerNode), nil, C.int64_t(nTasks))
-	var cpu, mem, wall C.int32_t
-	var k C.uint16_t
-	if err := check(C.fit_job_demand(&r, &cpu, &mem, &wall, &k)); err != nil {
-		return Demand{}, err
-	}
-	return Demand{Priority: priority, CPU: int32(cpu), MemMiB: int32(mem), GPU: 0,
-		WallMin: wallMin, Part: part, NodesK: uint16(k)}, nil
 }

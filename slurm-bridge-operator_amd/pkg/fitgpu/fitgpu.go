@@ -91,10 +91,12 @@ func (e *Engine) LoadNodes(n Nodes) error {
 		return check(C.fit_load_nodes(e.ctx, 0, nil, nil, nil, nil, nil))
 	}
 	// slices of plain integers: no Go pointers inside, the library copies and does not retain
-	return check(C.fit_load_nodes(e.ctx, C.int32_t(cnt),
+	rc := C.fit_load_nodes(e.ctx, C.int32_t(cnt),
 		(*C.int32_t)(unsafe.Pointer(&n.CPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.MemFreeMiB[0])),
 		(*C.int32_t)(unsafe.Pointer(&n.GPUFree[0])), (*C.int32_t)(unsafe.Pointer(&n.AvailMin[0])),
-		(*C.uint32_t)(unsafe.Pointer(&n.PartMask[0]))))
+		(*C.uint32_t)(unsafe.Pointer(&n.PartMask[0])))
+	runtime.KeepAlive(e) // the finalizer must not destroy the context during the call
+	return check(rc)
 }
 
 // LoadPartitions takes parseResources' limits (pkg/slurm-agent/parse.go:111-190), -1 = UNLIMITED.
@@ -142,6 +144,7 @@ func (e *Engine) Place(j Jobs, kmax int) ([]int32, Stats, error) {
 		(*C.int32_t)(unsafe.Pointer(&j.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&j.GPU[0])),
 		(*C.int32_t)(unsafe.Pointer(&j.WallMin[0])), (*C.uint16_t)(unsafe.Pointer(&j.Part[0])),
 		nk, C.int32_t(kmax), (*C.int32_t)(unsafe.Pointer(&out[0])), &st)
+	runtime.KeepAlive(e)
 	return out, st, check(rc)
 }
 
@@ -150,6 +153,7 @@ func (e *Engine) Place(j Jobs, kmax int) ([]int32, Stats, error) {
 func (e *Engine) PartitionFree(p int) (cpu, memMiB, gpu int64, err error) {
 	var c, m, g C.int64_t
 	err = check(C.fit_partition_free(e.ctx, C.int32_t(p), &c, &m, &g))
+	runtime.KeepAlive(e)
 	return int64(c), int64(m), int64(g), err
 }
 
@@ -195,6 +199,7 @@ func (e *Engine) PlaceBackfill(j Jobs) (node, start []int32, st Stats, err error
 		(*C.int32_t)(unsafe.Pointer(&j.MemMiB[0])), (*C.int32_t)(unsafe.Pointer(&j.GPU[0])),
 		(*C.int32_t)(unsafe.Pointer(&j.WallMin[0])), (*C.uint16_t)(unsafe.Pointer(&j.Part[0])),
 		(*C.int32_t)(unsafe.Pointer(&node[0])), (*C.int32_t)(unsafe.Pointer(&start[0])), &st)
+	runtime.KeepAlive(e)
 	return node, start, st, check(rc)
 }
 
@@ -238,4 +243,108 @@ func IngestNodes(text string, partitions []string) (Nodes, []string, error) {
 		}
 	}
 	return n, out, nil
+}
+
+// ---- CreatePod call site (include/fitgpu.h): every rule is in C; Go only marshals strings --------
+
+// PodLabels holds the sbo.kubecluster.org/<key> label values newSubmitRequestForPod reads
+// (pkg/slurm-virtual-kubelet/provider.go:74-123, keys pkg/common/labels.go:9-14); nil = absent.
+type PodLabels struct {
+	Nodes, CpusPerTask, MemPerCpu, NtasksPerNode, Array, Ntasks *string
+}
+
+func cstr(s *string) *C.char {
+	if s == nil {
+		return nil
+	}
+	return C.CString(*s)
+}
+
+// PodDemand derives a pod's admission requests from its labels and sbatch script (fit_pod_demand):
+// the script's #SBATCH header under the labels, the operator's defaults, one request per array
+// task that may run at once.
+func PodDemand(l PodLabels, script string, part uint16, priority int64) ([]Demand, error) {
+	fields := []*string{l.Nodes, l.CpusPerTask, l.MemPerCpu, l.NtasksPerNode, l.Array, l.Ntasks}
+	cs := make([]*C.char, len(fields))
+	for i, f := range fields {
+		cs[i] = cstr(f)
+		if cs[i] != nil {
+			defer C.free(unsafe.Pointer(cs[i]))
+		}
+	}
+	lab := C.fit_pod_labels{nodes: cs[0], cpus_per_task: cs[1], mem_per_cpu: cs[2],
+		ntasks_per_node: cs[3], array: cs[4], ntasks: cs[5]}
+	sc := C.CString(script)
+	defer C.free(unsafe.Pointer(sc))
+	n := C.fit_pod_demand(&lab, sc, C.uint16_t(part), C.int64_t(priority), nil, 0)
+	if err := check(n); err != nil {
+		return nil, err
+	}
+	reqs := make([]C.fit_admit_req, int(n))
+	if err := check(C.fit_pod_demand(&lab, sc, C.uint16_t(part), C.int64_t(priority), &reqs[0], n)); err != nil {
+		return nil, err
+	}
+	out := make([]Demand, len(reqs))
+	for i, r := range reqs {
+		out[i] = Demand{Priority: int64(r.priority), CPU: int32(r.cpu), MemMiB: int32(r.mem_mib),
+			GPU: int32(r.gpu), WallMin: int32(r.wall_min), Part: uint16(r.part), NodesK: uint16(r.nodes_k)}
+	}
+	return out, nil
+}
+
+// ScriptWithNodelist forwards the engine's nodes to slurmctld: the script with
+// `#SBATCH --nodelist=` at the end of its #SBATCH header (fit_script_with_nodelist).
+func ScriptWithNodelist(script string, names []string, nodes []int32) (string, error) {
+	if len(nodes) == 0 {
+		return script, nil
+	}
+	blob := make([]byte, 0, 16*len(names)+1)
+	for _, nm := range names {
+		blob = append(append(blob, nm...), 0)
+	}
+	blob = append(blob, 0)
+	cb := C.CBytes(blob)
+	defer C.free(cb)
+	sc := C.CString(script)
+	defer C.free(unsafe.Pointer(sc))
+	out := make([]byte, len(script)+32+len(blob)+1)
+	rc := C.fit_script_with_nodelist(sc, (*C.char)(cb), C.int32_t(len(names)),
+		(*C.int32_t)(unsafe.Pointer(&nodes[0])), C.int32_t(len(nodes)),
+		(*C.char)(unsafe.Pointer(&out[0])), C.int32_t(len(out)))
+	if err := check(rc); err != nil {
+		return "", err
+	}
+	return string(out[:int(rc)]), nil
+}
+
+// PartitionLimits converts a ResourcesResponse (workload.proto:137-148) into LoadPartitions' limits.
+func PartitionLimits(wallTimeS, cpuPerNode, memPerNode int64) (maxTimeMin, maxCPUs, maxMemMiB int32, err error) {
+	var t, c, m C.int32_t
+	err = check(C.fit_partition_limits(C.int64_t(wallTimeS), C.int64_t(cpuPerNode), C.int64_t(memPerNode), &t, &c, &m))
+	return int32(t), int32(c), int32(m), err
+}
+
+// ProtoNode is one workload.Node (workload.proto:165-174).
+type ProtoNode struct {
+	Cpus, Memory, Gpus, AlloCpus, AlloMemory, AlloGpus int64
+}
+
+// NodeColumns turns NodesResponse rows into a node table (free = total − alloc), every node in
+// the partitions of partMask.
+func NodeColumns(nodes []ProtoNode, partMask uint32) (Nodes, error) {
+	n := len(nodes)
+	t := Nodes{make([]int32, n), make([]int32, n), make([]int32, n), make([]int32, n), make([]uint32, n)}
+	if n == 0 {
+		return t, nil
+	}
+	rows := make([]C.fit_node, n)
+	for i, x := range nodes {
+		rows[i] = C.fit_node{cpus: C.int64_t(x.Cpus), memory: C.int64_t(x.Memory), gpus: C.int64_t(x.Gpus),
+			allo_cpus: C.int64_t(x.AlloCpus), allo_memory: C.int64_t(x.AlloMemory), allo_gpus: C.int64_t(x.AlloGpus)}
+	}
+	rc := C.fit_node_columns(&rows[0], C.int32_t(n), C.uint32_t(partMask),
+		(*C.int32_t)(unsafe.Pointer(&t.CPUFree[0])), (*C.int32_t)(unsafe.Pointer(&t.MemFreeMiB[0])),
+		(*C.int32_t)(unsafe.Pointer(&t.GPUFree[0])), (*C.int32_t)(unsafe.Pointer(&t.AvailMin[0])),
+		(*C.uint32_t)(unsafe.Pointer(&t.PartMask[0])))
+	return t, check(rc)
 }

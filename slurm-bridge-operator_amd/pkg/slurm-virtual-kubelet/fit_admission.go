@@ -1,13 +1,20 @@
 // fit_admission.go — the call sites of SURVEY.md §8 a10 / b2 / f4: the file a maintainer adds to
 // the reference's package pkg/slurm-virtual-kubelet (package slurm_virtual_kubelet, next to
-// provider.go and node.go).  Not compiled in this repo's image (no Go toolchain); the C++ side
-// it calls (fit_admitter, include/fitgpu.h) is tested on the GPU by tests/test_admit_gpu.py.
+// provider.go and node.go).  Not compiled in this repo's image (no Go toolchain).  It holds no
+// rule of its own: labels and script go to fit_pod_demand, the decision comes back through
+// fit_script_with_nodelist, limits and node rows through fit_partition_limits / fit_node_columns
+// (include/fitgpu.h "CreatePod call site") — all of which the tests call (tests/test_callsite.py,
+// tests/test_admit_gpu.py).
 //
 // What changes, behind the unchanged interfaces (nodeutil.Provider, workload.proto):
-//   - CreatePod (provider.go:35-60) asks the engine for a node before SubmitJob.  The 10
+//   - CreatePod (provider.go:35-60) asks the engine for nodes before SubmitJob.  The 10
 //     PodSyncWorkers' concurrent calls are coalesced by fitgpu.Admitter into one fit_place per
-//     batch, in pod-creation order.  A pod that does not fit now gets an error, and the library
-//     retries it later (the same contract as a failed SubmitJob).
+//     batch, in pod-creation order; an array job's tasks are admitted all or nothing.  A pod that
+//     does not fit now gets an error, and the library retries it later (the same contract as a
+//     failed SubmitJob).  A placed pod's script carries `#SBATCH --nodelist=` so slurmctld runs it
+//     where the engine reserved it (SubmitJobRequest.script, workload.proto:66).
+//   - The reservation lives until the pod's job runs (Confirm, from the status poll) or the pod is
+//     deleted / its submission fails (Release); node-table reloads re-apply open reservations.
 //   - GetPartitionCapacity (node.go:169-199) reports the engine's allocation-aware free capacity
 //     instead of the allocation-blind sum (which also adds AlloCpus into the GPU count).
 //   - The one-minute timer in NotifyNodeStatus (provider.go:470-488) becomes a ticker that
@@ -21,22 +28,25 @@ import (
 	"sync"
 	"time"
 
+	"github.com/chriskery/slurm-bridge-operator/apis/kubecluster.org/v1alpha1"
 	"github.com/chriskery/slurm-bridge-operator/pkg/common"
 	"github.com/chriskery/slurm-bridge-operator/pkg/fitgpu"
 	"github.com/chriskery/slurm-bridge-operator/pkg/workload"
 	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/api/resource"
+	"k8s.io/apimachinery/pkg/types"
 	"k8s.io/klog/v2"
 )
 
 // FitAdmission holds the engine of one virtual kubelet (one Slurm partition per VK:
-// KubeletServer.SlurmPartition).  The node table is that partition's nodes, in the order of its
-// Partition RPC, every node in partition 0.
+// KubeletServer.SlurmPartition, pkg/configurator/configurator.go:151-171).  The node table is that
+// partition's nodes, in the order of its Partition RPC, every node in partition 0.
 type FitAdmission struct {
-	adm   *fitgpu.Admitter
-	eng   *fitgpu.Engine
-	mu    sync.Mutex // nodes / names
-	names []string   // node id -> Slurm node name
+	adm     *fitgpu.Admitter
+	eng     *fitgpu.Engine
+	mu      sync.Mutex           // names / tickets
+	names   []string             // node id -> Slurm node name
+	tickets map[types.UID][]int64 // open reservations per pod
 }
 
 // NewFitAdmission creates the engine on GPU `device` and loads the partition's limits and nodes.
@@ -51,15 +61,12 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (
 		return nil, err
 	}
 	// parseResources' limits after the agent's override merge (pkg/slurm-agent/parse.go:111-190,
-	// api/slurm.go:297-341); -1 (UNLIMITED) or an unset 0 → no limit
-	limit := func(v int64) int32 {
-		if v <= 0 {
-			return -1
-		}
-		return int32(v)
+	// api/slurm.go:297-341), converted by fit_partition_limits
+	maxTime, maxCPUs, maxMem, err := fitgpu.PartitionLimits(res.WallTime, res.CpuPerNode, res.MemPerNode)
+	if err == nil {
+		err = eng.LoadPartitions([]int32{maxTime}, []int32{maxCPUs}, []int32{maxMem})
 	}
-	maxTime := limit(res.WallTime / 60) // seconds → minutes
-	if err := eng.LoadPartitions([]int32{maxTime}, []int32{limit(res.CpuPerNode)}, []int32{limit(res.MemPerNode)}); err != nil {
+	if err != nil {
 		eng.Close()
 		return nil, err
 	}
@@ -68,7 +75,7 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (
 		eng.Close()
 		return nil, err
 	}
-	f := &FitAdmission{adm: adm, eng: eng}
+	f := &FitAdmission{adm: adm, eng: eng, tickets: map[types.UID][]int64{}}
 	if err := f.Refresh(ctx, vk); err != nil {
 		f.Close()
 		return nil, err
@@ -76,8 +83,8 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (
 	return f, nil
 }
 
-// Refresh reloads the node table: Partition → Nodes RPCs, free = total − alloc per node
-// (workload.proto:165-174).
+// Refresh reloads the node table: Partition → Nodes RPCs → fit_node_columns (free = total −
+// alloc per node, workload.proto:165-174).  Open reservations are re-applied by the admitter.
 func (f *FitAdmission) Refresh(ctx context.Context, vk *SlurmVirtualKubelet) error {
 	pr, err := vk.SlurmClient.Partition(ctx, &workload.PartitionRequest{Partition: vk.KubeletServer.SlurmPartition})
 	if err != nil {
@@ -87,15 +94,14 @@ func (f *FitAdmission) Refresh(ctx context.Context, vk *SlurmVirtualKubelet) err
 	if err != nil {
 		return err
 	}
-	n := len(nr.Nodes)
-	t := fitgpu.Nodes{CPUFree: make([]int32, n), MemFreeMiB: make([]int32, n), GPUFree: make([]int32, n),
-		AvailMin: make([]int32, n), PartMask: make([]uint32, n)}
-	for i, node := range nr.Nodes {
-		t.CPUFree[i] = int32(node.Cpus - node.AlloCpus)
-		t.MemFreeMiB[i] = int32(node.Memory - node.AlloMemory)
-		t.GPUFree[i] = int32(node.Gpus - node.AlloGpus)
-		t.AvailMin[i] = 1<<31 - 1
-		t.PartMask[i] = 1
+	rows := make([]fitgpu.ProtoNode, len(nr.Nodes))
+	for i, n := range nr.Nodes {
+		rows[i] = fitgpu.ProtoNode{Cpus: n.Cpus, Memory: n.Memory, Gpus: n.Gpus,
+			AlloCpus: n.AlloCpus, AlloMemory: n.AlloMemory, AlloGpus: n.AlloGpus}
+	}
+	t, err := fitgpu.NodeColumns(rows, 1)
+	if err != nil {
+		return err
 	}
 	f.mu.Lock()
 	defer f.mu.Unlock()
@@ -111,69 +117,132 @@ func (f *FitAdmission) Close() {
 	f.eng.Close()
 }
 
-func labelInt(pod *v1.Pod, key string) int64 {
-	v, err := strconv.ParseInt(pod.Labels[key], 10, 64)
-	if err != nil {
-		return 0
+func podLabels(pod *v1.Pod) fitgpu.PodLabels {
+	get := func(k string) *string {
+		if v, ok := pod.Labels[k]; ok {
+			return &v
+		}
+		return nil
 	}
-	return v
+	return fitgpu.PodLabels{
+		Nodes: get(common.LabelsResourceRequestNodes), CpusPerTask: get(common.LabelsResourceRequestCpusPerTask),
+		MemPerCpu: get(common.LabelsResourceRequestMemPerCpu), NtasksPerNode: get(common.LabelsResourceRequestNTasksPerNode),
+		Array: get(common.LabelsResourceRequestArray), Ntasks: get(common.LabelsResourceRequestNTasks),
+	}
 }
 
-// admit places one pod; called by CreatePod before SubmitJob.  nil = the pod has nodes.
-func (f *FitAdmission) admit(pod *v1.Pod) error {
-	d, err := fitgpu.DemandFromLabels(
-		labelInt(pod, common.LabelsResourceRequestNodes), labelInt(pod, common.LabelsResourceRequestCpusPerTask),
-		labelInt(pod, common.LabelsResourceRequestMemPerCpu), labelInt(pod, common.LabelsResourceRequestNTasksPerNode),
-		labelInt(pod, common.LabelsResourceRequestNTasks), 0, 0, pod.CreationTimestamp.UnixNano())
+// admit places one pod; called by CreatePodWithFit before SubmitJob.  Returns the script to
+// submit (with the engine's nodes for a non-array job) and the pod's reservations.
+func (f *FitAdmission) admit(pod *v1.Pod) (string, []int64, error) {
+	script := pod.Spec.Containers[0].Command[0] // validateCreatePod checked the shape
+	ds, err := fitgpu.PodDemand(podLabels(pod), script, 0, pod.CreationTimestamp.UnixNano())
 	if err != nil {
-		return err
+		return "", nil, err
 	}
-	a, err := f.adm.Admit(d)
+	as, err := f.adm.AdmitGroup(ds)
 	if err != nil {
-		return err
+		return "", nil, err
 	}
 	switch {
-	case a.Placed():
-		f.mu.Lock()
-		names := make([]string, 0, len(a.Nodes))
-		for _, id := range a.Nodes {
-			if int(id) < len(f.names) {
-				names = append(names, f.names[id])
-			}
+	case as[0].Placed(): // all or nothing: every task has its nodes
+		tickets := make([]int64, len(as))
+		for i, a := range as {
+			tickets[i] = a.Ticket
 		}
+		if _, isArray := pod.Labels[common.LabelsResourceRequestArray]; isArray {
+			// one sbatch for every task: a --nodelist would pin all of them to every listed node;
+			// the reservations still gate the capacity
+			return script, tickets, nil
+		}
+		f.mu.Lock()
+		names := f.names
 		f.mu.Unlock()
-		klog.Infof("pod %s/%s fits on %v (batch %d, %d pods)", pod.Namespace, pod.Name, names, a.Batch, a.BatchJobs)
-		return nil
-	case a.Nodes[0] == fitgpu.Rejected:
-		return fmt.Errorf("pod %s/%s exceeds the partition's limits", pod.Namespace, pod.Name)
+		pinned, err := fitgpu.ScriptWithNodelist(script, names, as[0].Nodes)
+		if err != nil {
+			f.release(tickets)
+			return "", nil, err
+		}
+		klog.Infof("pod %s/%s fits on %v (batch %d, %d requests)", pod.Namespace, pod.Name, as[0].Nodes, as[0].Batch, as[0].BatchJobs)
+		return pinned, tickets, nil
+	case as[0].Nodes[0] == fitgpu.Rejected:
+		return "", nil, fmt.Errorf("pod %s/%s exceeds the partition's limits", pod.Namespace, pod.Name)
 	default: // Unplaced: no node has room now; the library retries the pod
-		return fmt.Errorf("pod %s/%s: no Slurm node of the partition fits it now", pod.Namespace, pod.Name)
+		return "", nil, fmt.Errorf("pod %s/%s: no Slurm node of the partition fits it now", pod.Namespace, pod.Name)
+	}
+}
+
+func (f *FitAdmission) release(tickets []int64) {
+	for _, t := range tickets {
+		if err := f.adm.Release(t); err != nil {
+			klog.Error(err)
+		}
 	}
 }
 
 // CreatePodWithFit is CreatePod (provider.go:35-60) with the engine's admission in front of
-// SubmitJob; provider.go's CreatePod calls it when s.fit != nil:
-//
-//	if s.fit != nil && needReconcile(pod) {
-//	        if err := s.fit.admit(pod); err != nil {
-//	                return err
-//	        }
-//	}
+// SubmitJob and its nodes in the submitted script; provider.go's CreatePod delegates to it when
+// s.fit != nil.
 func (s *SlurmVirtualKubeletProvider) CreatePodWithFit(ctx context.Context, pod *v1.Pod, f *FitAdmission) error {
-	if needReconcile(pod) {
-		if err := s.validateCreatePod(pod); err != nil {
-			return err
-		}
-		if err := f.admit(pod); err != nil {
-			return err
+	if !needReconcile(pod) {
+		return s.CreatePod(ctx, pod)
+	}
+	if err := s.validateCreatePod(pod); err != nil {
+		return err
+	}
+	script, tickets, err := f.admit(pod)
+	if err != nil {
+		return err
+	}
+	submitRequest := s.newSubmitRequestForPod(pod)
+	submitRequest.Script = script
+	submitJobResp, err := s.vk.SlurmClient.SubmitJob(ctx, submitRequest)
+	if err != nil {
+		f.release(tickets) // the job will not run: its capacity goes back
+		return err
+	}
+	f.mu.Lock()
+	f.tickets[pod.UID] = tickets
+	f.mu.Unlock()
+	s.vk.recorder.Eventf(pod, v1.EventTypeNormal, common.NewReason(v1alpha1.SlurmBridgeJobKind, common.SlurmBridgeJobCreatedReason),
+		"SlurmBridgeJob submit to the slurm-agent %s, job id is %d", s.vk.KubeletServer.AgentEndpoint, submitJobResp.JobId)
+	s.knownPods.Store(pod.UID, strconv.FormatInt(submitJobResp.GetJobId(), 10))
+	s.addAndUpdateSlurmJobInfo(pod, strconv.FormatInt(submitJobResp.GetJobId(), 10))
+	return nil
+}
+
+// ConfirmRunning is called from GetPodStatus (provider.go:195) once the pod's job has left the
+// pending state: Slurm counts its allocation from now on, so the reservation ends at the next
+// Refresh instead of being re-applied.
+func (f *FitAdmission) ConfirmRunning(pod *v1.Pod, phase v1.PodPhase) {
+	if phase == v1.PodPending {
+		return
+	}
+	f.mu.Lock()
+	tickets := f.tickets[pod.UID]
+	delete(f.tickets, pod.UID)
+	f.mu.Unlock()
+	for _, t := range tickets {
+		if err := f.adm.Confirm(t); err != nil {
+			klog.Error(err)
 		}
 	}
-	return s.CreatePod(ctx, pod)
+}
+
+// DeletePodWithFit is DeletePod (provider.go:156-181) plus the release of a reservation the pod
+// still holds (deleted before its job ran).
+func (s *SlurmVirtualKubeletProvider) DeletePodWithFit(ctx context.Context, pod *v1.Pod, f *FitAdmission) error {
+	f.mu.Lock()
+	tickets := f.tickets[pod.UID]
+	delete(f.tickets, pod.UID)
+	f.mu.Unlock()
+	f.release(tickets)
+	return s.DeletePod(ctx, pod)
 }
 
 // PartitionCapacityFromEngine replaces GetPartitionCapacity's sum (node.go:169-199) with the
-// engine's free columns after the admitted pods.  Units as the reference: memory quantity in
-// bytes from MiB.
+// engine's free columns after the admitted pods.  Memory is reported as MiB << 20 bytes — a
+// deliberate departure from the reference's mem*(2<<10) (node.go:193, MiB × 2048), which matches
+// neither the node's MiB nor the pods' KiB-as-bytes requests (pod.go:160).
 func (f *FitAdmission) PartitionCapacityFromEngine() (v1.ResourceList, error) {
 	cpu, mem, gpu, err := f.adm.PartitionFree(0)
 	if err != nil {
