@@ -1,0 +1,755 @@
+/* oracle/cpu_fast.c — like-for-like CPU baselines (BENCH / TEST INFRASTRUCTURE: bench.py's
+ * cpu_baseline leg and tests/ only; never linked into or called by the product).
+ *
+ * VERDICT r02 asked for CPU variants that do what the GPU does, so that "GPU ÷ CPU" compares
+ * algorithms on equal terms (results identical to ref_place / ref_place_tl, tests/test_cpu_baseline.py):
+ *
+ *   cpu_place_split   BASELINE.md:22's "fair multi-core CPU variant": every job's argmin split over
+ *                     all threads (each owns a contiguous share of the component's nodes, SoA,
+ *                     vectorised), one spin barrier per job, the serial commit done by the owner
+ *                     of the chosen node.  Components one after another.
+ *   cpu_place_rounds  the GPU's own algorithm (oracle/round_model.c) made fast:
+ *                     per component, windows of jobs scanned against the round-start state
+ *                     keeping each job's 16 smallest keys and the bound B, then a serial commit
+ *                     over a dirty set (128 nodes) with the same stop rules.  Components run on
+ *                     separate threads when there are at least as many as threads; otherwise one
+ *                     component at a time with the window scan split over all threads.
+ *   cpu_place_tl_rle  SPEC §2b on run-length timelines (the GPU's layout) instead of the dense
+ *                     slot walk of ref_key_tl: earliest start by walking runs, column ceilings
+ *                     as a prefilter, reservations split / merge runs; components on threads.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fitref.h"
+
+#define KINF UINT64_MAX
+
+/* ------------------------------------------------------------------------------ helpers */
+typedef struct {
+    int32_t nc, comp_of_part[32];
+    int32_t *nodes, *nb, *jobs, *jb;  /* node ids / job ids grouped by component */
+} groups_t;
+
+static int gfind(int* par, int x) {
+    while (par[x] != x) x = par[x] = par[par[x]];
+    return x;
+}
+
+static int build_groups(groups_t* G, int32_t n, const uint32_t* mask, int32_t p, const int32_t* mt,
+                        const int32_t* mc, const int32_t* mm, int32_t j, const int32_t* cpu,
+                        const int32_t* mem, const int32_t* wall, const uint16_t* part, int32_t* out) {
+    int par[32], used[32] = {0}, root[32];
+    for (int i = 0; i < 32; i++) par[i] = i, root[i] = -1;
+    for (int32_t x = 0; x < n; x++)
+        for (uint32_t m = mask[x]; m; m &= m - 1) {
+            int a = gfind(par, __builtin_ctz(mask[x])), b = gfind(par, __builtin_ctz(m));
+            used[__builtin_ctz(m)] = 1;
+            if (a != b) par[a > b ? a : b] = a < b ? a : b;
+        }
+    G->nc = 0;
+    for (int q = 0; q < 32; q++) {
+        G->comp_of_part[q] = -1;
+        if (!used[q]) continue;
+        int r = gfind(par, q);
+        if (root[r] < 0) root[r] = G->nc++;
+        G->comp_of_part[q] = root[r];
+    }
+    G->nb = calloc((size_t)G->nc + 1, sizeof(int32_t));
+    G->jb = calloc((size_t)G->nc + 1, sizeof(int32_t));
+    G->nodes = malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    G->jobs = malloc(sizeof(int32_t) * (size_t)(j > 0 ? j : 1));
+    int32_t* fill = malloc(sizeof(int32_t) * ((size_t)G->nc + 1));
+    if (!G->nb || !G->jb || !G->nodes || !G->jobs || !fill) {
+        free(fill);
+        return -1;
+    }
+    for (int32_t x = 0; x < n; x++)
+        if (mask[x]) G->nb[G->comp_of_part[__builtin_ctz(mask[x])] + 1]++;
+    for (int k = 0; k < G->nc; k++) G->nb[k + 1] += G->nb[k];
+    memcpy(fill, G->nb, sizeof(int32_t) * ((size_t)G->nc + 1));
+    for (int32_t x = 0; x < n; x++)
+        if (mask[x]) G->nodes[fill[G->comp_of_part[__builtin_ctz(mask[x])]]++] = x;
+    for (int32_t q = 0; q < j; q++) {
+        const int pq = part[q];
+        out[q] = -1;
+        if (pq >= p || (mt[pq] >= 0 && wall[q] > mt[pq]) || (mc[pq] >= 0 && cpu[q] > mc[pq]) ||
+            (mm[pq] >= 0 && mem[q] > mm[pq])) {
+            out[q] = -2;
+            continue;
+        }
+        if (pq < 32 && G->comp_of_part[pq] >= 0) G->jb[G->comp_of_part[pq] + 1]++;
+    }
+    for (int k = 0; k < G->nc; k++) G->jb[k + 1] += G->jb[k];
+    memcpy(fill, G->jb, sizeof(int32_t) * ((size_t)G->nc + 1));
+    for (int32_t q = 0; q < j; q++)
+        if (out[q] != -2 && part[q] < 32 && G->comp_of_part[part[q]] >= 0)
+            G->jobs[fill[G->comp_of_part[part[q]]]++] = q;
+    free(fill);
+    return 0;
+}
+
+static void free_groups(groups_t* G) {
+    free(G->nodes);
+    free(G->nb);
+    free(G->jobs);
+    free(G->jb);
+}
+
+/* sense-reversing spin barrier (the per-job barrier of the split variant: microseconds matter) */
+typedef struct {
+    volatile int32_t count, sense;
+    int32_t n;
+} spin_barrier;
+
+static void spin_wait(spin_barrier* b, int* local_sense) {
+    *local_sense = !*local_sense;
+    if (__atomic_add_fetch(&b->count, 1, __ATOMIC_ACQ_REL) == b->n) {
+        __atomic_store_n(&b->count, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&b->sense, *local_sense, __ATOMIC_RELEASE);
+    } else {
+        while (__atomic_load_n(&b->sense, __ATOMIC_ACQUIRE) != *local_sense) __builtin_ia32_pause();
+    }
+}
+
+/* SoA key of one position (SPEC §2 key; position = node id) */
+static inline uint64_t soa_key(int32_t cf, int32_t mf, int32_t gf, int32_t av, uint32_t mk, int32_t id,
+                               int32_t c, int32_t m, int32_t g, int32_t w, uint32_t pbit) {
+    const int32_t dc = cf - c, dm = mf - m, dg = gf - g, da = av - w;
+    const int ok = ((dc | dm | dg | da) >= 0) & ((mk & pbit) != 0);
+    uint32_t gr = (uint32_t)dg, cr = (uint32_t)dc, mr = (uint32_t)dm >> 10;
+    gr = gr > 255u ? 255u : gr;
+    cr = cr > 4095u ? 4095u : cr;
+    mr = mr > 4095u ? 4095u : mr;
+    const uint64_t key = ((uint64_t)((gr << 24) | (cr << 12) | mr) << 32) | (uint32_t)id;
+    return ok ? key : KINF;
+}
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static uint64_t range_min(int32_t lo, int32_t hi, const int32_t* cf, const int32_t* mf, const int32_t* gf,
+                          const int32_t* av, const uint32_t* mk, const int32_t* id, int32_t c, int32_t m,
+                          int32_t g, int32_t w, uint32_t pbit) {
+    uint64_t best = KINF;
+    for (int32_t i = lo; i < hi; i++) {
+        const uint64_t k = soa_key(cf[i], mf[i], gf[i], av[i], mk[i], id[i], c, m, g, w, pbit);
+        best = k < best ? k : best;
+    }
+    return best;
+}
+
+typedef struct {  /* one component's node table as SoA, positions in id order */
+    int32_t len, *cf, *mf, *gf, *av, *id;
+    uint32_t* mk;
+} soa_t;
+
+static int soa_load(soa_t* s, const groups_t* G, int k, const int32_t* cpu_free, const int32_t* mem_free,
+                    const int32_t* gpu_free, const int32_t* avail, const uint32_t* mask) {
+    const int32_t nb = G->nb[k], len = G->nb[k + 1] - nb;
+    s->len = len;
+    s->cf = malloc(sizeof(int32_t) * (size_t)(len > 0 ? len : 1) * 5);
+    s->mk = malloc(sizeof(uint32_t) * (size_t)(len > 0 ? len : 1));
+    if (!s->cf || !s->mk) return -1;
+    s->mf = s->cf + len;
+    s->gf = s->mf + len;
+    s->av = s->gf + len;
+    s->id = s->av + len;
+    for (int32_t i = 0; i < len; i++) {
+        const int32_t x = G->nodes[nb + i];
+        s->id[i] = x;
+        s->cf[i] = cpu_free[x];
+        s->mf[i] = mem_free[x];
+        s->gf[i] = gpu_free[x];
+        s->av[i] = avail[x];
+        s->mk[i] = mask[x];
+    }
+    return 0;
+}
+
+static void soa_store(soa_t* s, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free) {
+    for (int32_t i = 0; i < s->len; i++) {
+        cpu_free[s->id[i]] = s->cf[i];
+        mem_free[s->id[i]] = s->mf[i];
+        gpu_free[s->id[i]] = s->gf[i];
+    }
+    free(s->cf);
+    free(s->mk);
+}
+
+static int32_t soa_pos(const soa_t* s, int32_t x) { /* ids ascend */
+    int32_t lo = 0, hi = s->len - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (s->id[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* ------------------------------------------------------------------- split-argmin variant */
+typedef struct {
+    const groups_t* G;
+    soa_t* comp;            /* current component */
+    const int32_t *cpu, *mem, *gpu, *wall;
+    const uint16_t* part;
+    int32_t* out;
+    int32_t threads;
+    uint64_t best[2][256];  /* per thread, double-buffered by job parity */
+    spin_barrier bar;
+    int32_t k;              /* current component; -1 = done */
+    int64_t placed, evals;
+} split_t;
+
+static void split_component(split_t* T, int tid, int* sense) {
+    const soa_t* s = T->comp;
+    const groups_t* G = T->G;
+    const int32_t lo = (int32_t)((int64_t)s->len * tid / T->threads);
+    const int32_t hi = (int32_t)((int64_t)s->len * (tid + 1) / T->threads);
+    for (int32_t t = G->jb[T->k], par = 0; t < G->jb[T->k + 1]; t++, par ^= 1) {
+        const int32_t q = G->jobs[t];
+        T->best[par][tid] = range_min(lo, hi, s->cf, s->mf, s->gf, s->av, s->mk, s->id, T->cpu[q], T->mem[q],
+                                      T->gpu[q], T->wall[q], 1u << T->part[q]);
+        spin_wait(&T->bar, sense);
+        uint64_t b = KINF;  /* every thread reduces (no second barrier); the owner commits */
+        for (int i = 0; i < T->threads; i++) b = T->best[par][i] < b ? T->best[par][i] : b;
+        if (b == KINF) continue;
+        const int32_t x = (int32_t)(uint32_t)b, at = soa_pos(s, x);
+        if (at >= lo && at < hi) {
+            s->cf[at] -= T->cpu[q];
+            s->mf[at] -= T->mem[q];
+            s->gf[at] -= T->gpu[q];
+        }
+        if (tid == 0) {
+            T->out[q] = x;
+            T->placed++;
+        }
+    }
+}
+
+typedef struct {
+    split_t* T;
+    int tid;
+} split_arg;
+
+static void* split_worker(void* a) {
+    split_t* T = ((split_arg*)a)->T;
+    const int tid = ((split_arg*)a)->tid;
+    int sense = 0;
+    for (;;) {
+        spin_wait(&T->bar, &sense);  /* thread 0 has set up the next component */
+        if (T->k < 0) break;
+        split_component(T, tid, &sense);
+        spin_wait(&T->bar, &sense);  /* component done */
+    }
+    return NULL;
+}
+
+int cpu_place_split(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free,
+                    const int32_t* avail_min, const uint32_t* part_mask, int32_t p, const int32_t* max_time,
+                    const int32_t* max_cpus, const int32_t* max_mem, int32_t j, const int32_t* cpu,
+                    const int32_t* mem, const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                    int32_t* out, int64_t* stats, int32_t threads) {
+    if (n < 0 || j < 0 || p < 0 || p > 32) return -1;
+    for (int32_t q = 0; q < j; q++)
+        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0) return -1;
+    groups_t G;
+    memset(&G, 0, sizeof G);
+    if (build_groups(&G, n, part_mask, p, max_time, max_cpus, max_mem, j, cpu, mem, wall, part, out)) {
+        free_groups(&G);
+        return -1;
+    }
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    split_t* T = calloc(1, sizeof *T);
+    T->G = &G;
+    T->cpu = cpu;
+    T->mem = mem;
+    T->gpu = gpu;
+    T->wall = wall;
+    T->part = part;
+    T->out = out;
+    T->threads = threads;
+    T->bar.n = threads;
+    pthread_t th[256];
+    split_arg args[256];
+    for (int i = 1; i < threads; i++) {
+        args[i] = (split_arg){T, i};
+        pthread_create(&th[i], NULL, split_worker, &args[i]);
+    }
+    int sense = 0;
+    soa_t s;
+    for (int k = 0; k < G.nc; k++) {
+        soa_load(&s, &G, k, cpu_free, mem_free, gpu_free, avail_min, part_mask);
+        T->comp = &s;
+        T->k = k;
+        T->evals += (int64_t)(G.jb[k + 1] - G.jb[k]) * s.len;
+        spin_wait(&T->bar, &sense);
+        split_component(T, 0, &sense);
+        spin_wait(&T->bar, &sense);
+        soa_store(&s, cpu_free, mem_free, gpu_free);
+    }
+    T->k = -1;
+    spin_wait(&T->bar, &sense);
+    for (int i = 1; i < threads; i++) pthread_join(th[i], NULL);
+    int64_t rejected = 0;
+    for (int32_t q = 0; q < j; q++) rejected += out[q] == -2;
+    if (stats) {
+        stats[0] = T->placed;
+        stats[1] = j - T->placed - rejected;
+        stats[2] = rejected;
+        stats[3] = T->evals;
+    }
+    free(T);
+    free_groups(&G);
+    return 0;
+}
+
+/* ----------------------------------------------------- the GPU's round algorithm on the CPU */
+#define RK 16       /* candidates kept per job (one slice: the whole component) */
+#define RUCAP 128   /* dirty nodes per round */
+#define RWMIN 256
+#define RWMAX 8192
+
+typedef struct {
+    soa_t* s;
+    const int32_t *jobs, *cpu, *mem, *gpu, *wall;
+    const uint16_t* part;
+    uint64_t* cand;  /* [w][RK] */
+    uint64_t* bnd;   /* [w] */
+    int32_t w;
+    volatile int32_t next;
+    int64_t evals;
+} scan_t;
+
+/* top-RK keys of job q over the component (sorted), and the bound: the RK-th key when more than
+ * RK nodes fit (every node outside the list is above it), else INF */
+static void scan_job(const soa_t* s, int32_t c, int32_t m, int32_t g, int32_t w, uint32_t pbit, uint64_t* cl,
+                     uint64_t* bound) {
+    for (int i = 0; i < RK; i++) cl[i] = KINF;
+    int64_t feas = 0;
+    enum { BLK = 256 };
+    uint64_t kb[BLK];
+    for (int32_t b0 = 0; b0 < s->len; b0 += BLK) {
+        const int32_t b1 = b0 + BLK < s->len ? b0 + BLK : s->len;
+        for (int32_t i = b0; i < b1; i++)  /* vectorisable */
+            kb[i - b0] = soa_key(s->cf[i], s->mf[i], s->gf[i], s->av[i], s->mk[i], s->id[i], c, m, g, w, pbit);
+        for (int32_t i = 0; i < b1 - b0; i++) {
+            const uint64_t k = kb[i];
+            if (k == KINF) continue;
+            feas++;
+            if (k >= cl[RK - 1]) continue;
+            int a = RK - 1;
+            while (a > 0 && cl[a - 1] > k) {
+                cl[a] = cl[a - 1];
+                a--;
+            }
+            cl[a] = k;
+        }
+    }
+    *bound = feas > RK ? cl[RK - 1] : KINF;
+}
+
+static void* scan_worker(void* a) {
+    scan_t* S = a;
+    for (;;) {
+        const int32_t t = __atomic_fetch_add(&S->next, 1, __ATOMIC_RELAXED);
+        if (t >= S->w) break;
+        const int32_t q = S->jobs[t];
+        scan_job(S->s, S->cpu[q], S->mem[q], S->gpu[q], S->wall[q], 1u << S->part[q], S->cand + (size_t)t * RK,
+                 S->bnd + t);
+    }
+    return NULL;
+}
+
+/* one component, all rounds; `threads` > 1 splits each window's scan over threads */
+static void rounds_component(soa_t* s, const int32_t* jobs, int32_t nj, const int32_t* cpu, const int32_t* mem,
+                             const int32_t* gpu, const int32_t* wall, const uint16_t* part, int32_t* out,
+                             int threads, int64_t* placed, int64_t* evals) {
+    uint64_t* cand = malloc(sizeof(uint64_t) * RWMAX * RK);
+    uint64_t* bnd = malloc(sizeof(uint64_t) * RWMAX);
+    int32_t* slot_of = malloc(sizeof(int32_t) * (size_t)(s->len > 0 ? s->len : 1));
+    for (int32_t i = 0; i < s->len; i++) slot_of[i] = -1;
+    int32_t up[RUCAP], ucf[RUCAP], umf[RUCAP], ugf[RUCAP], uav[RUCAP], uid[RUCAP];
+    uint32_t umk[RUCAP];
+    int32_t cur = 0, win = RWMIN;
+    while (cur < nj) {
+        const int32_t w = win < nj - cur ? win : nj - cur;
+        scan_t S = {s, jobs + cur, cpu, mem, gpu, wall, part, cand, bnd, w, 0, 0};
+        if (threads > 1) {
+            pthread_t th[256];
+            for (int i = 1; i < threads; i++) pthread_create(&th[i], NULL, scan_worker, &S);
+            scan_worker(&S);
+            for (int i = 1; i < threads; i++) pthread_join(th[i], NULL);
+        } else {
+            scan_worker(&S);
+        }
+        *evals += (int64_t)w * s->len;
+        int32_t nu = 0, done = 0, stop = 0;
+        for (int32_t t = 0; t < w; t++) {
+            const int32_t q = jobs[cur + t];
+            const uint32_t pbit = 1u << part[q];
+            const uint64_t* cl = cand + (size_t)t * RK;
+            uint64_t e = KINF;  /* smallest clean candidate (its key is current) */
+            for (int i = 0; i < RK && cl[i] != KINF; i++)
+                if (slot_of[soa_pos(s, (int32_t)(uint32_t)cl[i])] < 0) {
+                    e = cl[i];
+                    break;
+                }
+            uint64_t d = KINF;  /* smallest current key over the dirty set */
+            int32_t ds = -1;
+            for (int32_t u = 0; u < nu; u++) {
+                const uint64_t k = soa_key(ucf[u], umf[u], ugf[u], uav[u], umk[u], uid[u], cpu[q], mem[q], gpu[q],
+                                           wall[q], pbit);
+                if (k < d) d = k, ds = u;
+            }
+            uint64_t best;
+            if (e != KINF) best = e < d ? e : d;
+            else if (bnd[t] == KINF || d <= bnd[t]) best = d;
+            else {
+                stop = 1;  /* a node outside the list could win: rescan next round */
+                break;
+            }
+            if (best == KINF) {
+                done++;
+                continue;
+            }
+            int32_t u = best == d ? ds : -1;
+            if (u < 0) {
+                if (nu == RUCAP) {
+                    stop = 2;
+                    break;
+                }
+                const int32_t at = soa_pos(s, (int32_t)(uint32_t)best);
+                u = nu++;
+                up[u] = at;
+                ucf[u] = s->cf[at];
+                umf[u] = s->mf[at];
+                ugf[u] = s->gf[at];
+                uav[u] = s->av[at];
+                umk[u] = s->mk[at];
+                uid[u] = s->id[at];
+                slot_of[at] = u;
+            }
+            ucf[u] -= cpu[q];
+            umf[u] -= mem[q];
+            ugf[u] -= gpu[q];
+            out[q] = uid[u];
+            ++*placed;
+            done++;
+        }
+        for (int32_t u = 0; u < nu; u++) {
+            s->cf[up[u]] = ucf[u];
+            s->mf[up[u]] = umf[u];
+            s->gf[up[u]] = ugf[u];
+            slot_of[up[u]] = -1;
+        }
+        cur += done;
+        int32_t nw = stop ? 2 * done : 2 * w;
+        win = nw < RWMIN ? RWMIN : nw > RWMAX ? RWMAX : nw;
+    }
+    free(cand);
+    free(bnd);
+    free(slot_of);
+}
+
+typedef struct {
+    const groups_t* G;
+    int32_t *cpu_free, *mem_free, *gpu_free;
+    const int32_t* avail;
+    const uint32_t* mask;
+    const int32_t *cpu, *mem, *gpu, *wall;
+    const uint16_t* part;
+    int32_t* out;
+    volatile int32_t next;
+    int64_t placed, evals;
+    pthread_mutex_t mu;
+} rounds_t;
+
+static void* rounds_worker(void* a) {
+    rounds_t* T = a;
+    int64_t placed = 0, evals = 0;
+    for (;;) {
+        const int32_t k = __atomic_fetch_add(&T->next, 1, __ATOMIC_RELAXED);
+        if (k >= T->G->nc) break;
+        soa_t s;
+        soa_load(&s, T->G, k, T->cpu_free, T->mem_free, T->gpu_free, T->avail, T->mask);
+        rounds_component(&s, T->G->jobs + T->G->jb[k], T->G->jb[k + 1] - T->G->jb[k], T->cpu, T->mem, T->gpu,
+                         T->wall, T->part, T->out, 1, &placed, &evals);
+        soa_store(&s, T->cpu_free, T->mem_free, T->gpu_free);  /* distinct nodes per component */
+    }
+    pthread_mutex_lock(&T->mu);
+    T->placed += placed;
+    T->evals += evals;
+    pthread_mutex_unlock(&T->mu);
+    return NULL;
+}
+
+int cpu_place_rounds(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free,
+                     const int32_t* avail_min, const uint32_t* part_mask, int32_t p, const int32_t* max_time,
+                     const int32_t* max_cpus, const int32_t* max_mem, int32_t j, const int32_t* cpu,
+                     const int32_t* mem, const int32_t* gpu, const int32_t* wall, const uint16_t* part,
+                     int32_t* out, int64_t* stats, int32_t threads) {
+    if (n < 0 || j < 0 || p < 0 || p > 32) return -1;
+    for (int32_t q = 0; q < j; q++)
+        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0) return -1;
+    groups_t G;
+    memset(&G, 0, sizeof G);
+    if (build_groups(&G, n, part_mask, p, max_time, max_cpus, max_mem, j, cpu, mem, wall, part, out)) {
+        free_groups(&G);
+        return -1;
+    }
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    rounds_t T;
+    memset(&T, 0, sizeof T);
+    T.G = &G;
+    T.cpu_free = cpu_free;
+    T.mem_free = mem_free;
+    T.gpu_free = gpu_free;
+    T.avail = avail_min;
+    T.mask = part_mask;
+    T.cpu = cpu;
+    T.mem = mem;
+    T.gpu = gpu;
+    T.wall = wall;
+    T.part = part;
+    T.out = out;
+    pthread_mutex_init(&T.mu, NULL);
+    if (G.nc >= threads) {  /* whole components per thread */
+        pthread_t th[256];
+        for (int i = 1; i < threads; i++) pthread_create(&th[i], NULL, rounds_worker, &T);
+        rounds_worker(&T);
+        for (int i = 1; i < threads; i++) pthread_join(th[i], NULL);
+    } else {  /* one component at a time, each window's scan on every thread */
+        for (int k = 0; k < G.nc; k++) {
+            soa_t s;
+            soa_load(&s, &G, k, cpu_free, mem_free, gpu_free, avail_min, part_mask);
+            rounds_component(&s, G.jobs + G.jb[k], G.jb[k + 1] - G.jb[k], cpu, mem, gpu, wall, part, out, threads,
+                             &T.placed, &T.evals);
+            soa_store(&s, cpu_free, mem_free, gpu_free);
+        }
+    }
+    int64_t rejected = 0;
+    for (int32_t q = 0; q < j; q++) rejected += out[q] == -2;
+    if (stats) {
+        stats[0] = T.placed;
+        stats[1] = j - T.placed - rejected;
+        stats[2] = rejected;
+        stats[3] = T.evals;
+    }
+    pthread_mutex_destroy(&T.mu);
+    free_groups(&G);
+    return 0;
+}
+
+/* ------------------------------------------------------- SPEC §2b on run-length timelines */
+typedef struct {
+    int32_t end, c, m, g;
+} run_t;
+
+typedef struct {
+    run_t* r;         /* runs, canonical, last end = H */
+    int32_t n, cap;
+    int32_t cc, cm, cg;  /* column ceilings (maxima as built; reservations only lower values) */
+} rle_t;
+
+static void rle_from_dense(rle_t* L, const int32_t* row, int32_t H) {
+    L->cap = 16;
+    L->r = malloc(sizeof(run_t) * (size_t)L->cap);
+    L->n = 0;
+    L->cc = L->cm = L->cg = -1;
+    for (int32_t t = 0; t < H; t++) {
+        const int32_t c = row[t * 3], m = row[t * 3 + 1], g = row[t * 3 + 2];
+        if (L->n && L->r[L->n - 1].c == c && L->r[L->n - 1].m == m && L->r[L->n - 1].g == g) {
+            L->r[L->n - 1].end = t + 1;
+            continue;
+        }
+        if (L->n == L->cap) L->r = realloc(L->r, sizeof(run_t) * (size_t)(L->cap *= 2));
+        L->r[L->n++] = (run_t){t + 1, c, m, g};
+        L->cc = c > L->cc ? c : L->cc;
+        L->cm = m > L->cm ? m : L->cm;
+        L->cg = g > L->cg ? g : L->cg;
+    }
+}
+
+/* earliest start of a d-slot window holding (c, m, g), best fit among that start's nodes: key as
+ * ref_key_tl (start << 54 | score << 22 | node); stops once every start is later than `lim` */
+static uint64_t rle_key(const rle_t* L, int32_t x, int32_t c, int32_t m, int32_t g, int32_t d, int32_t H,
+                        int32_t lim) {
+    int32_t a = 0, ra = -1, mc = 0, mm = 0, mg = 0;
+    for (int32_t i = 0; i < L->n; i++) {
+        const run_t* u = &L->r[i];
+        if (u->c >= c && u->m >= m && u->g >= g) {
+            if (ra < 0) ra = a, mc = u->c, mm = u->m, mg = u->g;
+            else {
+                mc = u->c < mc ? u->c : mc;
+                mm = u->m < mm ? u->m : mm;
+                mg = u->g < mg ? u->g : mg;
+            }
+            if (u->end - ra >= d) {
+                uint32_t gr = (uint32_t)(mg - g), cr = (uint32_t)(mc - c), mr = (uint32_t)(mm - m) >> 10;
+                gr = gr > 255u ? 255u : gr;
+                cr = cr > 4095u ? 4095u : cr;
+                mr = mr > 4095u ? 4095u : mr;
+                return ((uint64_t)(uint32_t)ra << 54) | ((uint64_t)((gr << 24) | (cr << 12) | mr) << 22) |
+                       (uint32_t)x;
+            }
+            if (ra > lim) return KINF;
+        } else {
+            ra = -1;
+            if (u->end + d > H || u->end > lim) return KINF;
+        }
+        a = u->end;
+    }
+    return KINF;
+}
+
+static void rle_reserve(rle_t* L, int32_t s, int32_t e, int32_t c, int32_t m, int32_t g) {
+    /* split at s and e, lower [s, e), merge equal neighbours */
+    run_t* o = malloc(sizeof(run_t) * (size_t)(L->n + 2));
+    int32_t no = 0, a = 0;
+    for (int32_t i = 0; i < L->n; i++) {
+        const run_t u = L->r[i];
+        if (u.end <= s || a >= e) {
+            o[no++] = u;
+        } else {
+            if (a < s) o[no++] = (run_t){s, u.c, u.m, u.g};
+            o[no++] = (run_t){u.end < e ? u.end : e, u.c - c, u.m - m, u.g - g};
+            if (u.end > e) o[no++] = u;
+        }
+        a = u.end;
+    }
+    int32_t k = 0;
+    for (int32_t i = 0; i < no; i++) {
+        if (k && o[k - 1].c == o[i].c && o[k - 1].m == o[i].m && o[k - 1].g == o[i].g) o[k - 1].end = o[i].end;
+        else o[k++] = o[i];
+    }
+    if (k > L->cap) {
+        L->r = realloc(L->r, sizeof(run_t) * (size_t)k);
+        L->cap = k;
+    }
+    memcpy(L->r, o, sizeof(run_t) * (size_t)k);
+    L->n = k;
+    free(o);
+}
+
+typedef struct {
+    const groups_t* G;
+    rle_t* L;  /* by node id */
+    int32_t H, slot_min;
+    const uint32_t* mask;
+    const int32_t *cpu, *mem, *gpu, *wall;
+    const uint16_t* part;
+    int32_t *out, *outs;
+    volatile int32_t next;
+    int64_t placed, evals;
+    pthread_mutex_t mu;
+} rle_job_t;
+
+static void* rle_worker(void* a) {
+    rle_job_t* T = a;
+    const groups_t* G = T->G;
+    int64_t placed = 0, evals = 0;
+    for (;;) {
+        const int32_t k = __atomic_fetch_add(&T->next, 1, __ATOMIC_RELAXED);
+        if (k >= G->nc) break;
+        const int32_t* id = G->nodes + G->nb[k];
+        const int32_t len = G->nb[k + 1] - G->nb[k];
+        for (int32_t t = G->jb[k]; t < G->jb[k + 1]; t++) {
+            const int32_t q = G->jobs[t];
+            const int32_t d = ref_slots(T->wall[q], T->slot_min);
+            const int32_t c = T->cpu[q], m = T->mem[q], g = T->gpu[q];
+            const uint32_t pbit = 1u << T->part[q];
+            uint64_t best = KINF;
+            if (d <= T->H)
+                for (int32_t i = 0; i < len; i++) {
+                    const int32_t x = id[i];
+                    const rle_t* L = &T->L[x];
+                    if (!(T->mask[x] & pbit) || c > L->cc || m > L->cm || g > L->cg) continue;
+                    const int32_t lim = best == KINF ? T->H : (int32_t)(best >> 54);
+                    const uint64_t key = rle_key(L, x, c, m, g, d, T->H, lim);
+                    best = key < best ? key : best;
+                }
+            evals += len;
+            if (best == KINF) continue;
+            const int32_t x = (int32_t)(best & 0x3fffffu), s = (int32_t)(best >> 54);
+            rle_reserve(&T->L[x], s, s + d, c, m, g);
+            T->out[q] = x;
+            T->outs[q] = s;
+            placed++;
+        }
+    }
+    pthread_mutex_lock(&T->mu);
+    T->placed += placed;
+    T->evals += evals;
+    pthread_mutex_unlock(&T->mu);
+    return NULL;
+}
+
+/* Same contract as cpu_place_tl (dense [n][H][3] in, updated in place). */
+int cpu_place_tl_rle(int32_t n, int32_t H, int32_t slot_min, int32_t* tl, const uint32_t* part_mask, int32_t p,
+                     const int32_t* max_time, const int32_t* max_cpus, const int32_t* max_mem, int32_t j,
+                     const int32_t* cpu, const int32_t* mem, const int32_t* gpu, const int32_t* wall,
+                     const uint16_t* part, int32_t* out_node, int32_t* out_start, int64_t* stats, int32_t threads) {
+    if (n < 0 || n > (1 << 22) || j < 0 || p < 0 || p > 32 || H < 1 || H > 1024 || slot_min < 1) return -1;
+    for (int32_t q = 0; q < j; q++)
+        if (cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0) return -1;
+    groups_t G;
+    memset(&G, 0, sizeof G);
+    if (build_groups(&G, n, part_mask, p, max_time, max_cpus, max_mem, j, cpu, mem, wall, part, out_node)) {
+        free_groups(&G);
+        return -1;
+    }
+    for (int32_t q = 0; q < j; q++) out_start[q] = -1;
+    rle_t* L = calloc((size_t)(n > 0 ? n : 1), sizeof(rle_t));
+    for (int32_t x = 0; x < n; x++)
+        if (part_mask[x]) rle_from_dense(&L[x], tl + (int64_t)x * H * 3, H);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    rle_job_t T;
+    memset(&T, 0, sizeof T);
+    T.G = &G;
+    T.L = L;
+    T.H = H;
+    T.slot_min = slot_min;
+    T.mask = part_mask;
+    T.cpu = cpu;
+    T.mem = mem;
+    T.gpu = gpu;
+    T.wall = wall;
+    T.part = part;
+    T.out = out_node;
+    T.outs = out_start;
+    pthread_mutex_init(&T.mu, NULL);
+    pthread_t th[256];
+    for (int i = 1; i < threads; i++) pthread_create(&th[i], NULL, rle_worker, &T);
+    rle_worker(&T);
+    for (int i = 1; i < threads; i++) pthread_join(th[i], NULL);
+    for (int32_t x = 0; x < n; x++) {  /* back to the dense layout */
+        if (!part_mask[x]) continue;
+        int32_t a = 0;
+        for (int32_t i = 0; i < L[x].n; i++) {
+            for (int32_t t = a; t < L[x].r[i].end; t++) {
+                int32_t* v = tl + ((int64_t)x * H + t) * 3;
+                v[0] = L[x].r[i].c;
+                v[1] = L[x].r[i].m;
+                v[2] = L[x].r[i].g;
+            }
+            a = L[x].r[i].end;
+        }
+        free(L[x].r);
+    }
+    free(L);
+    int64_t rejected = 0;
+    for (int32_t q = 0; q < j; q++) rejected += out_node[q] == -2;
+    if (stats) {
+        stats[0] = T.placed;
+        stats[1] = j - T.placed - rejected;
+        stats[2] = rejected;
+        stats[3] = T.evals;
+    }
+    pthread_mutex_destroy(&T.mu);
+    free_groups(&G);
+    return 0;
+}

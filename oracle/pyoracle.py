@@ -20,7 +20,7 @@ def lib():
     if _LIB is None:
         path = os.path.join(_HERE, "liboracle.so")
         srcs = [os.path.join(_HERE, f) for f in ("fitref.c", "fitref_tl.c", "round_model.c", "cpu_baseline.c",
-                                                 "fitref.h", "Makefile")]
+                                                 "cpu_fast.c", "fitref.h", "Makefile")]
         if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
             subprocess.check_call(["make", "-s", "-C", _HERE])
         _LIB = C.CDLL(path)
@@ -131,14 +131,17 @@ def ref_place_tl(nodes, tline, jobs, parts, tl=None):
 
 
 # ---- fair CPU baselines (oracle/cpu_baseline.c; bench.py cpu_baseline leg) -----------------------
-def cpu_place(nodes, jobs, parts, threads: int = 1):
-    """Component-aware sequential best fit (k = 1), components on `threads` threads.  Same result
-    as ref_place.  Returns (out[J] int32, stats dict, final (cpu, mem, gpu))."""
+def cpu_place(nodes, jobs, parts, threads: int = 1, variant: str = "component"):
+    """Sequential best fit (k = 1) on the CPU, same result as ref_place.  variant: "component"
+    (oracle/cpu_baseline.c: components on `threads` threads), "split" (every job's argmin split over
+    the threads, BASELINE.md:22) or "rounds" (the GPU's candidate-list + dirty-set algorithm,
+    oracle/cpu_fast.c).  Returns (out[J] int32, stats dict, final (cpu, mem, gpu))."""
     cf, mf, gf, av, mk, pt, jb, jp, _ = _prep(nodes, jobs, parts)
     out = np.empty(jobs.j, np.int32)
     st = np.zeros(4, np.int64)
     I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
-    rc = lib().cpu_place(
+    fn = {"component": lib().cpu_place, "split": lib().cpu_place_split, "rounds": lib().cpu_place_rounds}[variant]
+    rc = fn(
         I32(nodes.n), _p(cf, I32), _p(mf, I32), _p(gf, I32), _p(av, I32), _p(mk, U32),
         I32(parts.p), _p(pt[0], I32), _p(pt[1], I32), _p(pt[2], I32),
         I32(jobs.j), _p(jb[0], I32), _p(jb[1], I32), _p(jb[2], I32), _p(jb[3], I32), _p(jp, U16),
@@ -148,8 +151,9 @@ def cpu_place(nodes, jobs, parts, threads: int = 1):
     return out, dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3])), (cf, mf, gf)
 
 
-def cpu_place_tl(nodes, tline, jobs, parts, threads: int = 1, tl=None):
-    """Component-aware SPEC §2b backfill on `threads` threads.  Same result as ref_place_tl."""
+def cpu_place_tl(nodes, tline, jobs, parts, threads: int = 1, tl=None, rle: bool = False):
+    """Component-aware SPEC §2b backfill on `threads` threads (dense slot walk, or run-length
+    timelines with rle=True: oracle/cpu_fast.c).  Same result as ref_place_tl."""
     tl = ref_build_timeline(nodes, tline) if tl is None else np.ascontiguousarray(tl, np.int32).copy()
     I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
     mk = np.ascontiguousarray(nodes.part_mask, np.uint32)
@@ -160,7 +164,7 @@ def cpu_place_tl(nodes, tline, jobs, parts, threads: int = 1, tl=None):
     node = np.empty(jobs.j, np.int32)
     start = np.empty(jobs.j, np.int32)
     st = np.zeros(4, np.int64)
-    rc = lib().cpu_place_tl(I32(nodes.n), I32(tline.slots), I32(tline.slot_min), _p(tl, I32), _p(mk, U32),
+    rc = (lib().cpu_place_tl_rle if rle else lib().cpu_place_tl)(I32(nodes.n), I32(tline.slots), I32(tline.slot_min), _p(tl, I32), _p(mk, U32),
                             I32(parts.p), *(_p(a, I32) for a in pt), I32(jobs.j), *(_p(a, I32) for a in jb),
                             _p(jp, U16), _p(node, I32), _p(start, I32), _p(st, C.c_int64), I32(threads))
     if rc != 0:

@@ -878,6 +878,13 @@ __global__ __launch_bounds__(64) void k_commit_tl(
     if (threadIdx.x == 0) res[c] = r;
 }
 
+#ifndef FIT_TL_MW
+#define FIT_TL_MW 1  // 0: the single-wave committer (commit_tl_window) in k_engine_tl too
+#endif
+}  // namespace fitgpu
+#include "fit_commit_tl_mw.h"
+namespace fitgpu {
+
 // ------------------------------------------------------------------------------ k_engine_tl
 // The whole backfill placement in ONE launch, on k_engine's protocol
 // (fit_persistent.hip, fit_engine_ctl.h): blocks [0, C) are committers — one wave each runs the
@@ -898,8 +905,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     const int lane = threadIdx.x & 63;
 
     if ((int)blockIdx.x < ncomp) {
-        // ================================================================ committer (1 wave)
-        if (threadIdx.x >= 64) return;
+        // ================================================================ committer
+        // FIT_TL_MW: wave 0 runs the round protocol (publish the window's tiles), then all 8
+        // waves commit it (fit_commit_tl_mw.h: wave 0 decides, waves 1..7 pre-resolve);
+        // otherwise wave 0 alone runs both (commit_tl_window).
+        __shared__ int s_fail;
+        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        if (!FIT_TL_MW && wave != 0) return;
         const int c = blockIdx.x;
         const CompState S = cs[c];
         int32_t cursor = S.jstart, win = S.wmin;
@@ -915,38 +927,56 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             P.se = S.se;
             P.nslice = S.nslice;
             P.sub = S.sub;
+            P.ks = S.ks;
             P.jbase = cursor;
             P.w = w;
             P.blk0 = 0;
             P.cand_off = S.cand_off;
             P.slot0 = S.slot0;
+            P.k0 = 0;
             const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            // the previous window's tiles (also those past its stop) must all be complete before
-            // their buffers and counters are reused
-            if (!wait_tiles(ctl, c, target)) {
+            if (wave == 0) {
+                // the previous window's tiles (also those past its stop) must all be complete
+                // before their buffers and counters are reused
+                bool f = !wait_tiles(ctl, c, target);
+                const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
+                if (lane == 0) plans[c] = P;
+                for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+                for (unsigned i = lane; i < ntj; i += 64)
+                    __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                release_agent();  // plan, bound / counter reset and the last window's run lists
+                // the whole window's tiles up front (a committer wave publishing tiles as the
+                // commit reaches them put the ring stores on the commit chain: 169.5 -> 175 ms)
+                const unsigned ntiles = ntj * (unsigned)S.nslice;
+                engine_publish(ctl, ring, 0u, ntj, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                target += ntiles;
+                if (f && lane == 0) atomicOr(&ctl->error, 1u);
+                if (FIT_TL_MW) {
+                    acquire_agent();  // run lists written back by this block: CU-wide fresh view
+                    if (lane == 0) s_fail = f;
+                }
+                fail = f;
+            }
+            if (FIT_TL_MW) {
+                __syncthreads();
+                if (s_fail) break;  // block-uniform
+            } else if (fail) {
+                break;
+            }
+            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+            // committed while its tiles are scanned: per-tile readiness inside
+            const CommitResult r =
+                FIT_TL_MW ? commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
+                                                &ctl->tdone[c][0], (unsigned)S.nslice)
+                          : commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd, wjob, perm, out,
+                                                outs, H, R, &ctl->tdone[c][0], (unsigned)S.nslice);
+            if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
+            if (r.stop == 3) {
                 fail = true;
                 break;
             }
-            const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
-            if (lane == 0) plans[c] = P;
-            for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
-            for (unsigned i = lane; i < ntj; i += 64)
-                __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            release_agent();  // plan, bound / counter reset and the last window's run lists
-            // the whole window's tiles up front: this committer is one wave, and publishing tiles
-            // as its commit reaches them (as k_engine's helpers do) put the ring stores on the
-            // commit chain — measured 169.5 -> 175-176 ms (2 / 4 / 8 tiles ahead)
-            const unsigned ntiles = ntj * (unsigned)S.nslice;
-            engine_publish(ctl, ring, 0u, ntj, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
-            target += ntiles;
-            const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
-            // committed while its tiles are scanned: per-tile readiness inside
-            const CommitResult r = commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd,
-                                                       wjob, perm, out, outs, H, R,
-                                                       &ctl->tdone[c][0], (unsigned)S.nslice);
-            if (lane == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
-            if (r.stop == 3) {
-                fail = true;
+            if (r.done == 0) {  // the next round would rescan the same state: never progresses
+                if (threadIdx.x == 0) atomicOr(&ctl->error, 4u);
                 break;
             }
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -961,6 +991,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             const int nw = r.stop ? 2 * r.done : 2 * w;
             win = max(S.wmin, min(S.wmax, nw));
         }
+        if (wave != 0) return;
         if (fail && lane == 0) atomicOr(&ctl->error, 1u);
         release_agent();  // last window's run lists / placements (kernel end also flushes)
         if (lane == 0) {
@@ -1134,21 +1165,27 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg*
 }
 
 // k_engine_tl: the committer takes a whole CU's LDS (run lists of up to 64 runs stay in LDS; the
-// scan workers are mostly idle at one block per CU: DESIGN.md §3.8).
+// scan workers are mostly idle at one block per CU: DESIGN.md §3.8).  Regions are R + TL_PAD runs
+// apart with R + TL_PAD odd (an even multiple of 16 B puts the lanes' own-list reads on one bank).
 constexpr size_t TL_ENGINE_LDS = 160 * 1024;
+static size_t engine_tl_fixed(int32_t max_component_nodes) {
+    const size_t head = FIT_TL_MW ? tm_fixed_bytes() : sizeof(Seg) * TL_MAX_SLOTS;
+    return head + (size_t)((max_component_nodes + 31) / 32) * 4;
+}
 int engine_tl_runs(int32_t max_component_nodes) {
-    const size_t fixed = sizeof(Seg) * TL_MAX_SLOTS + (size_t)((max_component_nodes + 31) / 32) * 4;
+    const size_t fixed = engine_tl_fixed(max_component_nodes);
     if (fixed >= TL_ENGINE_LDS) return 0;
     const size_t fit = (TL_ENGINE_LDS - fixed) / ((sizeof(Seg) + sizeof(int4)) * TL_UCAP);
     if (fit <= (size_t)TL_PAD) return 0;
-    return (int)std::min<size_t>(2 * TL_PM_STEPS, fit - TL_PAD);  // regions are R + TL_PAD apart
+    int r = (int)std::min<size_t>(2 * TL_PM_STEPS, fit - TL_PAD);
+    if (((r + TL_PAD) & 1) == 0) --r;
+    return r;
 }
 
 size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
     const int runs = engine_tl_runs(max_component_nodes);
-    const size_t commit = sizeof(Seg) * TL_MAX_SLOTS +
-                          (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * (runs > 0 ? runs + TL_PAD : 0) +
-                          (size_t)((max_component_nodes + 31) / 32) * 4;
+    const size_t commit = engine_tl_fixed(max_component_nodes) +
+                          (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * (runs > 0 ? runs + TL_PAD : 0);
     const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16;
     return std::max(commit, scan);
 }
