@@ -94,9 +94,15 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5"],
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5", "admit"],
                     help="c3: BASELINE headline (100k x 1M); c3o: c3 + an all-nodes partition (one "
-                         "component); c5: c3 with a 1,024-slot backfill horizon")
+                         "component); c5: c3 with a 1,024-slot backfill horizon; admit: CreatePod "
+                         "admission latency (10 concurrent callers against the c3 node table)")
+    ap.add_argument("--repeats", type=int, default=3,
+                    help="timed runs of --steps steps each; value = their median (BASELINE.md:26)")
+    ap.add_argument("--no-shard-price", action="store_true",
+                    help="skip the one-GPU price of north_star's node-sharded layout (c3 / c3o)")
+    ap.add_argument("--admit-pods", type=int, default=300, help="admit: pods per caller thread")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-scale", type=float, default=1.0, help="scale the CPU-baseline samples (tests)")
     ap.add_argument("--no-device-path", action="store_true", help="skip the HBM-resident rate")
@@ -128,6 +134,10 @@ def _pinned(keep, a):
 
 def main():
     a = parse_args()
+    if a.workload == "admit":
+        import torch
+        torch.cuda.set_device(0)
+        return admission(a)
     import torch
     import torch.distributed as dist
 
@@ -212,15 +222,13 @@ def main():
 
     cdev = torch.device("cpu") if a.rehearse else dev  # gloo reduces CPU tensors
 
-    def timed(step):
-        for _ in range(a.warmup):
-            step()
+    def timed_once(step, steps):
         stats = []
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for _ in range(steps):
             stats.append(step())
         torch.cuda.synchronize()
         if world > 1:
@@ -232,12 +240,23 @@ def main():
             el = float(t.item())
         return el, stats
 
-    el, stats_host = timed(step_host)
+    def timed(step, repeats=None):
+        """W warmup steps, then `repeats` timed runs of exactly K steps each (barrier +
+        synchronize on both sides, max over ranks); returns the median run's time, its stats and
+        every run's time (BASELINE.md:26: median of 3)."""
+        for _ in range(a.warmup):
+            step()
+        runs = [timed_once(step, a.steps) for _ in range(max(1, repeats or a.repeats))]
+        order = sorted(range(len(runs)), key=lambda i: runs[i][0])
+        el, stats = runs[order[len(runs) // 2]]
+        return el, stats, [r[0] for r in runs]
+
+    el, stats_host, runs_host = timed(step_host)
     s0 = stats_host[-1]
     assert s0["placed"] + s0["unplaced"] + s0["rejected"] == jobs.j  # output sanity every run
     mult = world if weak else 1
     value = jobs.j * a.steps / el * mult
-    el_dev, stats = (None, stats_host) if a.no_device_path else timed(step_dev)
+    el_dev, stats, runs_dev = (None, stats_host, None) if a.no_device_path else timed(step_dev)
 
     agg = {k: sum(s[k] for s in stats) for k in ("rounds", "evals", "useful_evals", "ms_scan", "ms_commit",
                                                   "ms_exchange", "ms_device", "placed", "unplaced")}
@@ -280,6 +299,10 @@ def main():
                    "partitions": parts.p * mult, "per_gpu": {"nodes": nodes.n, "jobs": jobs.j} if weak else None,
                    **({"slots": tline.slots, "slot_min": tline.slot_min} if tl else {}),
                    "parallelism": used_mode, "components": stats[-1]["components"]},
+        "timing": {"repeats": len(runs_host), "statistic": "median (BASELINE.md:26)",
+                   "value_runs": [round(jobs.j * a.steps / r * mult, 1) for r in runs_host],
+                   "kernel_path_value_runs": [round(jobs.j * a.steps / r * mult, 1) for r in runs_dev] if runs_dev
+                   else None},
         "kernel_path_value": round(jobs.j * a.steps / el_dev * mult, 1) if el_dev else None,
         "kernel_path_ms_per_step": round(el_dev / a.steps * 1e3, 3) if el_dev else None,
         "placed_plus_unplaced_per_s": round(resolved * a.steps / el * mult, 1),
@@ -292,6 +315,9 @@ def main():
     }
     if cpu:
         line["speedup_vs_cpu"] = {v["kind"]: round(value / v["value"], 1) for v in cpu["variants"]}
+    if world == 1 and not tl and a.workload in ("c3", "c3o") and not a.no_shard_price:
+        line["node_sharding_1gpu"] = shard_price(Engine, FIT_SHARD_NODES, parts, h_nodes, h_jobs, h_out,
+                                                 kmax, el / a.steps * 1e3)
     if world > 1 and not weak and not a.no_weak_extra:
         # extra key: the same ranks, each placing its own 100k x 1M cluster shard (disjoint generator
         # slice, its own partitions; no collective in the data path), aggregate rate, host path
@@ -320,7 +346,7 @@ def main():
                 return weng.place_tl(wh_jobs, node=wh_out, start=wh_start)[2]
             return weng.place(wh_jobs, kmax=1, out=wh_out)[1]
 
-        wel, _ = timed(step_weak)
+        wel, _, _ = timed(step_weak)
         weng.close()
         line["weak_scaling"] = {"value": round(wj.j * a.steps / wel * world, 1), "unit": "placements/s",
                                 "ms_per_step": round(wel / a.steps * 1e3, 3), "scaling": "weak",
@@ -335,11 +361,103 @@ def main():
         dist.destroy_process_group()
 
 
+def shard_price(Engine, FIT_SHARD_NODES, parts, h_nodes, h_jobs, h_out, kmax, ms_default, steps=3):
+    """North_star's node-sharded layout priced on one GPU: the same
+    placement through the multi-rank code path at world 1 (FIT_FLAG_COLLECTIVES: a one-rank RCCL
+    communicator; per round the candidate allgather + u64 min-allreduce of the bounds, host-driven
+    rounds) against the default persistent engine."""
+    from fitgpu import FIT_FLAG_COLLECTIVES
+    e = Engine(device=0, shard_mode=FIT_SHARD_NODES, flags=FIT_FLAG_COLLECTIVES)
+    e.load_partitions(parts)
+    e.load_nodes(h_nodes)
+    e.place(h_jobs, kmax=kmax, out=h_out)  # warmup
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = None
+    for _ in range(steps):
+        e.load_nodes(h_nodes)
+        st = e.place(h_jobs, kmax=kmax, out=h_out)[1]
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    e.close()
+    return {"ms_per_step": round(ms, 3), "vs_default": round(ms / ms_default, 2), "steps": steps,
+            "rounds": st["rounds"], "ms_exchange": round(st["ms_exchange"], 3),
+            "path": "FIT_SHARD_NODES via FIT_FLAG_COLLECTIVES at world 1: host-driven rounds, RCCL allgather of "
+                    "the candidate sections + ncclMin of the bounds every round"}
+
+
+def admission(a):
+    """CreatePod admission latency: 10 threads — the virtual kubelet's
+    PodSyncWorkers (options/options.go:107), one pod per CreatePod (provider.go:35-60) — call
+    fit_admit against the 100k-node C3 table; per-pod latency (call to return) p50 / p99 and pods/s,
+    for the default coalescer (max_batch 1024, max_wait 2 ms: the Go call site's setting) and a
+    zero-wait one (a batch is whatever is queued when the coalescer wakes)."""
+    import threading
+
+    from fitgpu import Admitter, Engine, synth
+    nodes, jobs, parts = synth.make_config("c3")
+    callers, per = 10, a.admit_pods
+    out = {}
+    for name, mb, mw in (("max_wait_2ms", 1024, 2000), ("max_wait_0", 1024, 0)):
+        e = Engine(device=0)
+        e.load_partitions(parts)
+        adm = Admitter(e, max_batch=mb, max_wait_us=mw)
+        adm.load_nodes(nodes)
+        for i in range(20):  # warmup (first launches)
+            adm.admit(i, int(jobs.cpu[i]), int(jobs.mem[i]), int(jobs.gpu[i]), int(jobs.wall[i]), int(jobs.part[i]))
+        adm.load_nodes(nodes)
+        lat = [[] for _ in range(callers)]
+        batches = set()
+        bar = threading.Barrier(callers)
+
+        def worker(w):
+            bar.wait()
+            for i in range(per):
+                q = w * per + i
+                t = time.perf_counter()
+                r = adm.admit(q, int(jobs.cpu[q]), int(jobs.mem[q]), int(jobs.gpu[q]), int(jobs.wall[q]),
+                              int(jobs.part[q]))
+                lat[w].append(time.perf_counter() - t)
+                batches.add(r[1])
+
+        th = [threading.Thread(target=worker, args=(w,)) for w in range(callers)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        el = time.perf_counter() - t0
+        adm.close()
+        e.close()
+        us = np.sort(np.concatenate([np.array(x) for x in lat])) * 1e6
+        out[name] = {"pods_per_s": round(callers * per / el, 1), "p50_us": round(float(np.percentile(us, 50)), 1),
+                     "p99_us": round(float(np.percentile(us, 99)), 1), "max_us": round(float(us[-1]), 1),
+                     "batches": len(batches), "pods_per_batch": round(callers * per / max(len(batches), 1), 2)}
+    best = out["max_wait_0"]
+    line = {"metric": "CreatePod admission: pods/s and per-pod latency, 10 concurrent callers, 100k-node table",
+            "value": best["pods_per_s"], "unit": "pods/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "int32", "data": "synthetic c3 node table and job stream (fitgpu/synth.py)",
+            "config": {"workload": "admit", "nodes": nodes.n, "callers": callers, "pods": callers * per,
+                       "partitions": parts.p},
+            "policies": out,
+            "reference": "one SubmitJob per CreatePod on 10 PodSyncWorkers, no capacity check "
+                         "(provider.go:35-60, options/options.go:107)"}
+    print(json.dumps(line), flush=True)
+
+
 def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
-    """The CPU paths on this host (rank 0, N = 1), each on a bounded sample of the same workload:
-    the naive port (oracle/fitref*.c, every node per job, 1 thread), the component-aware scan
-    (oracle/cpu_baseline.c, 1 thread) and the same on CPU_THREADS threads (components in parallel).
-    Per-job cost is flat in J, so each sample's rate stands for the whole stream."""
+    """The CPU paths on this host (rank 0, N = 1), each on a bounded sample of the same workload
+    (per-job cost is flat in J, so each sample's rate stands for the whole stream):
+      naive-port                oracle/fitref*.c, every node per job, 1 thread (the SPEC as stated)
+      component-aware           oracle/cpu_baseline.c, own component's nodes, vectorised, 1 thread
+      same-algorithm            oracle/cpu_fast.c, the GPU's candidate-list + dirty-set rounds, 1 thread
+      split-argmin              BASELINE.md:22: each job's argmin over CPU_THREADS threads, serial commit
+      same-algorithm-multicore  the GPU's algorithm on CPU_THREADS threads
+      multicore                 component-aware, components on CPU_THREADS threads
+    backfill (c5): naive-port, component-aware (dense slot walk), run-length (the GPU's run lists,
+    1 thread) and multicore (run lists, components on threads).  The line's cpu_baseline object is
+    the fastest variant."""
     from fitgpu import synth
     from oracle import pyoracle as po
     threads = max(1, min(CPU_THREADS, os.cpu_count() or 1))
@@ -354,7 +472,7 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
     per_comp = nodes.n / max(ncomp, 1)
     par = min(threads, ncomp)
     if tline is not None:  # a timeline evaluation walks runs of slots: ~20x a plain fit eval
-        m_naive, m_comp = 1e8 / nodes.n, 1.5e7 / per_comp
+        m_naive, m_comp, m_rle = 1e8 / nodes.n, 1.5e7 / per_comp, 3e8 / per_comp
     else:
         m_naive, m_comp = 2e9 / nodes.n, 6e9 / per_comp
     m_mc = m_comp * par
@@ -362,14 +480,28 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
         runs = [("naive-port", 1, m_naive, lambda s: po.ref_place_tl(nodes, tline, s, parts)[2],
                  "oracle/fitref_tl.c ref_place_tl (SPEC §2b, dense timelines, every node per job)"),
                 ("component-aware", 1, m_comp, lambda s: po.cpu_place_tl(nodes, tline, s, parts, 1)[2],
-                 "oracle/cpu_baseline.c cpu_place_tl (own component's nodes only)"),
-                ("multicore", threads, m_mc, lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads)[2],
-                 f"oracle/cpu_baseline.c cpu_place_tl, {ncomp} components on {threads} threads")]
+                 "oracle/cpu_baseline.c cpu_place_tl (own component's nodes only, dense slot walk)"),
+                ("run-length", 1, m_rle, lambda s: po.cpu_place_tl(nodes, tline, s, parts, 1, rle=True)[2],
+                 "oracle/cpu_fast.c cpu_place_tl_rle (run-length timelines, the GPU's layout; 1 thread)"),
+                ("multicore", threads, m_rle * par,
+                 lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads, rle=True)[2],
+                 f"oracle/cpu_fast.c cpu_place_tl_rle, {ncomp} components on {threads} threads")]
     else:
+        # split-argmin: every job's scan split over the threads, one barrier per job
+        m_split = 3e9 / per_comp * max(1, min(threads, 4))
         runs = [("naive-port", 1, m_naive, lambda s: po.ref_place(nodes, s, parts)[1],
                  "oracle/fitref.c ref_place (C restatement of the scalar sequential path, every node per job)"),
                 ("component-aware", 1, m_comp, lambda s: po.cpu_place(nodes, s, parts, 1)[1],
                  "oracle/cpu_baseline.c cpu_place (own component's nodes only, vectorised scan)"),
+                ("same-algorithm", 1, m_comp, lambda s: po.cpu_place(nodes, s, parts, 1, "rounds")[1],
+                 "oracle/cpu_fast.c cpu_place_rounds (the GPU's candidate-list + dirty-set rounds, 1 thread)"),
+                ("split-argmin", threads, m_split, lambda s: po.cpu_place(nodes, s, parts, threads, "split")[1],
+                 f"oracle/cpu_fast.c cpu_place_split (BASELINE.md:22: each job's argmin over {threads} threads, "
+                 "serial commit)"),
+                ("same-algorithm-multicore", threads, m_comp * min(threads, 4),
+                 lambda s: po.cpu_place(nodes, s, parts, threads, "rounds")[1],
+                 f"oracle/cpu_fast.c cpu_place_rounds on {threads} threads ("
+                 + ("components on threads" if ncomp >= threads else "each window's scan over the threads") + ")"),
                 ("multicore", threads, m_mc, lambda s: po.cpu_place(nodes, s, parts, threads)[1],
                  f"oracle/cpu_baseline.c cpu_place, {ncomp} components on {threads} threads")]
     variants = []

@@ -332,8 +332,8 @@ static void scan_job(const soa_t* s, int32_t c, int32_t m, int32_t g, int32_t w,
     uint64_t kb[BLK];
     for (int32_t b0 = 0; b0 < s->len; b0 += BLK) {
         const int32_t b1 = b0 + BLK < s->len ? b0 + BLK : s->len;
-        for (int32_t i = b0; i < b1; i++)  /* vectorisable */
-            kb[i - b0] = soa_key(s->cf[i], s->mf[i], s->gf[i], s->av[i], s->mk[i], s->id[i], c, m, g, w, pbit);
+        for (int32_t i = b0; i < b1; i++)  /* vectorisable; low word = position (ids ascend with it) */
+            kb[i - b0] = soa_key(s->cf[i], s->mf[i], s->gf[i], s->av[i], s->mk[i], i, c, m, g, w, pbit);
         for (int32_t i = 0; i < b1 - b0; i++) {
             const uint64_t k = kb[i];
             if (k == KINF) continue;
@@ -370,7 +370,7 @@ static void rounds_component(soa_t* s, const int32_t* jobs, int32_t nj, const in
     uint64_t* bnd = malloc(sizeof(uint64_t) * RWMAX);
     int32_t* slot_of = malloc(sizeof(int32_t) * (size_t)(s->len > 0 ? s->len : 1));
     for (int32_t i = 0; i < s->len; i++) slot_of[i] = -1;
-    int32_t up[RUCAP], ucf[RUCAP], umf[RUCAP], ugf[RUCAP], uav[RUCAP], uid[RUCAP];
+    int32_t up[RUCAP], ucf[RUCAP], umf[RUCAP], ugf[RUCAP], uav[RUCAP], uid[RUCAP];  /* up: position */
     uint32_t umk[RUCAP];
     int32_t cur = 0, win = RWMIN;
     while (cur < nj) {
@@ -392,14 +392,14 @@ static void rounds_component(soa_t* s, const int32_t* jobs, int32_t nj, const in
             const uint64_t* cl = cand + (size_t)t * RK;
             uint64_t e = KINF;  /* smallest clean candidate (its key is current) */
             for (int i = 0; i < RK && cl[i] != KINF; i++)
-                if (slot_of[soa_pos(s, (int32_t)(uint32_t)cl[i])] < 0) {
+                if (slot_of[(uint32_t)cl[i]] < 0) {
                     e = cl[i];
                     break;
                 }
             uint64_t d = KINF;  /* smallest current key over the dirty set */
             int32_t ds = -1;
             for (int32_t u = 0; u < nu; u++) {
-                const uint64_t k = soa_key(ucf[u], umf[u], ugf[u], uav[u], umk[u], uid[u], cpu[q], mem[q], gpu[q],
+                const uint64_t k = soa_key(ucf[u], umf[u], ugf[u], uav[u], umk[u], up[u], cpu[q], mem[q], gpu[q],
                                            wall[q], pbit);
                 if (k < d) d = k, ds = u;
             }
@@ -420,7 +420,7 @@ static void rounds_component(soa_t* s, const int32_t* jobs, int32_t nj, const in
                     stop = 2;
                     break;
                 }
-                const int32_t at = soa_pos(s, (int32_t)(uint32_t)best);
+                const int32_t at = (int32_t)(uint32_t)best;
                 u = nu++;
                 up[u] = at;
                 ucf[u] = s->cf[at];
