@@ -132,6 +132,19 @@ __device__ __forceinline__ uint64_t tm_fit0(const Seg* L, const int4* PM, int cn
     return fit0 ? tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, pos) : KEY_INF;
 }
 
+#ifdef FIT_STAMPS
+// diagnostic build: g_tlst[comp][i] (fit_timeline.hip) — decider [0] record waits, [1] decision
+// (ring search + item merge), [2] exception path (walks, global lists), [3] new dirty copy,
+// [4] reservation + prefix minima, [5] jobs, [6] new dirty nodes, [7] round-end write-back,
+// [8] whole apply phase (copy + reservation + bookkeeping), [9] jobs that walked; helpers
+// [10] snapshot -> record cycles, [11] helper jobs
+#define TM_CLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define TM_ADD(i, x) D.acc[i] += (x)
+#else
+#define TM_CLK(v)
+#define TM_ADD(i, x)
+#endif
+
 // ------------------------------------------------------------------------------- helper
 struct TmJob {
     uint64_t kk, B;
@@ -172,6 +185,18 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         return true;
     };
     TmJob cur, nxt;
+#ifdef FIT_STAMPS
+    unsigned long long hs_acc = 0, hs_n = 0;
+    struct Flush {
+        unsigned long long &a, &n;
+        __device__ ~Flush() {
+            if ((threadIdx.x & 63) == 0) {
+                atomicAdd(&g_tlst[blockIdx.x & 63][10], a);
+                atomicAdd(&g_tlst[blockIdx.x & 63][11], n);
+            }
+        }
+    } flush{hs_acc, hs_n};
+#endif
     if (!load(t, cur)) return;
     for (;;) {
         if (t >= P.w) break;
@@ -191,6 +216,9 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
             for (int s = min(lag, 8); s > 0; --s) __builtin_amdgcn_s_sleep(2);
         }
         lds_acquire();
+#ifdef FIT_STAMPS
+        const unsigned long long hs0 = __builtin_amdgcn_s_memtime();
+#endif
         const int v = rfl((int32_t)(uint32_t)dn);
         const int nu = rfl((int32_t)(uint32_t)(dn >> 32));
         const JobRec& J = cur.J;
@@ -288,6 +316,10 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
             lds_release();  // items, stage and header before the ready word
             lds_st(&Rr->h.ready, (uint32_t)t + 1u);
         }
+#ifdef FIT_STAMPS
+        hs_acc += __builtin_amdgcn_s_memtime() - hs0;
+        ++hs_n;
+#endif
         (void)myitem;
         cur = nxt;
         t += TM_H;
@@ -337,6 +369,9 @@ struct TmDec {
     int t, nu, placed, stop;
     uint64_t gm;  // dirty slots whose list lives in the global slab
     bool exit;
+#ifdef FIT_STAMPS
+    unsigned long long acc[10];
+#endif
 };
 
 // Current key of job (jc..jd, jp) on a global-slab dirty list (lane 0 walks it; uniform result).
@@ -406,7 +441,10 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         d.w = __builtin_ctzll((__ballot(d.cand == d.bs) & 0xffull) | 0x100ull) & 7;
         return d;
     };
+    TM_CLK(c0);
     Dec d = decide(cur);
+    TM_CLK(c1);
+    TM_ADD(1, c1 - c0);
     const uint64_t B = ((uint64_t)cur.h3.y << 32) | cur.h3.x;
     int gslot = -1;  // winner: a global-slab dirty list that is not in the ring
     {
@@ -415,6 +453,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         const bool rec_missing = flag != (uint32_t)t + 1u;
         if (__builtin_expect(!D.exit && (rec_missing || need_walk || D.gm != 0ull), 0)) {
             if (rec_missing) {  // record t not complete when read: wait for it, read it again
+                TM_CLK(w0);
                 for (unsigned sp = 0;; ++sp) {
                     flag = lds_ld(&S->rec[t & (TM_R - 1)].h.ready);
                     if (flag == (uint32_t)t + 1u) break;
@@ -428,8 +467,11 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 }
                 lds_acquire();
                 tm_read_rec(&S->rec[t & (TM_R - 1)], lane & 7, cur);
+                TM_CLK(w1);
+                TM_ADD(0, w1 - w0);
                 d = decide(cur);
             }
+            TM_CLK(x0);
             if (!D.exit) {
                 const int32_t v = (int32_t)cur.h0.y;
                 const int32_t jc = (int32_t)cur.h1.x, jm = (int32_t)cur.h1.y, jg = (int32_t)cur.h1.z,
@@ -442,6 +484,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 // ring lists on LDS that fail at slot 0: a later start can still win only if the
                 // best so far starts later than 0 — walk them (wave-wide, one list at a time)
                 if (d.anywalk && (bm == KEY_INF || (bm >> 54) > 0)) {
+                    TM_ADD(9, 1);
                     const int32_t lim = bm == KEY_INF ? X.H : (int32_t)(bm >> 54);
                     const bool ok = live && !isg && (R.mask & jp) != 0u && jd <= X.H;
                     for (uint64_t m = __ballot(ok) & 0xffull; m; m &= m - 1) {
@@ -479,6 +522,8 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 d.bs = best;
                 d.w = __builtin_ctzll((__ballot(d.cand == d.bs) & 0xffull) | 0x100ull) & 7;
             }
+            TM_CLK(x1);
+            TM_ADD(2, x1 - x0);
         }
     }
     // stops: a node outside the candidate lists could win (rescan), or the dirty set is full
@@ -517,6 +562,10 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         orig = readlane((int32_t)cur.i0.w, w);
         mask = (uint32_t)readlane((int32_t)cur.i1.x, w);
     }
+    TM_CLK(a0);
+#ifdef FIT_STAMPS
+    unsigned long long a1 = a0;
+#endif
     if (placed) {
         Seg* const L = X.lr + slot * X.RS;
         int4* const PM = X.pmr + slot * X.RS;
@@ -544,7 +593,12 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             }
             if (glob) D.gm |= 1ull << slot;
             D.nu += 1;
+            TM_ADD(6, 1);
         }
+#ifdef FIT_STAMPS
+        a1 = __builtin_amdgcn_s_memtime();
+        TM_ADD(3, a1 - a0);
+#endif
         int nn;
         if (!glob) {
             nn = tl_reserve_lds(L, cnt, X.R, start, start + jd, jc, jm, jg);
@@ -567,6 +621,10 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             S->slot[slot].glob = glob ? 1 : 0;
         }
         cnt = nn;
+        {
+            TM_CLK(a2);
+            TM_ADD(4, a2 - a1);
+        }
         // ring: an older entry of the same slot dies; lane E takes job t
         R.job = (R.slot == slot) ? -1 : R.job;
         R.slot = writelane_c<E>(slot, R.slot);
@@ -595,6 +653,13 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         oq = -1;
     }
     D.t = t + (go ? 1 : 0);
+#ifdef FIT_STAMPS
+    {
+        TM_CLK(a3);
+        TM_ADD(8, a3 - a0);
+        TM_ADD(5, go ? 1 : 0);
+    }
+#endif
 }
 
 __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* Sin, Seg* lr_,
@@ -617,7 +682,8 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     TmShared* const S = X.S;
     const int lane = threadIdx.x & 63;
     __builtin_amdgcn_s_setprio(3);  // shares its SIMD with a helper wave
-    TmDec D{0, 0, 0, 0, 0ull, false};
+    TmDec D{};
+    D.exit = false;
     TmRing R{-1, 0xffffffffu, 0u, 0, -1, -1};
     int32_t oq = -1, on = -1, os = -1;
     TmRecRegs ra, rb;
@@ -658,6 +724,10 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
     lds_st(&S->halt, 1u);
+#ifdef FIT_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 10; ++i) atomicAdd(&g_tlst[blockIdx.x & 63][i], D.acc[i]);
+#endif
     return CommitResult{t, D.stop, D.nu, D.placed};
 }
 
@@ -702,11 +772,13 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
     __syncthreads();
     const CommitResult r{S->res[0], S->res[1], S->res[2], S->res[3]};
     // round end: LDS lists back to their slabs (the next scan reads them), headers for all
-    // (slot l by wave l & 7)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int lane = threadIdx.x & 63;
     // (slot l by wave l & 7; a global-slab list only by wave 0, which wrote it: its own stores are
     // ordered before its loads, another wave's L1 could hold the lines stale)
+#ifdef FIT_STAMPS
+    const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int l = 0; l < r.dirty; ++l) {
         const TmSlot s = S->slot[l];
         const bool gl = rfl(s.glob) != 0;
@@ -728,6 +800,9 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
         if (lane == 0) hdr[p].cnt = n;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+#ifdef FIT_STAMPS
+    if (threadIdx.x == 0) atomicAdd(&g_tlst[blockIdx.x & 63][7], __builtin_amdgcn_s_memtime() - e0);
+#endif
     __syncthreads();
     if (S->fail) return CommitResult{r.done, 3, r.dirty, r.placed};
     return r;

@@ -23,12 +23,22 @@ with Engine() as e:
 print({k: st[k] for k in ("ms_total", "ms_scan", "ms_commit", "rounds", "stops_rescan", "stops_dirty", "placed")})
 tot = [sum(buf[c * 12 + i] for c in range(64)) for i in range(12)]
 j = max(tot[5], 1)
-names = ["clean", "dirty-eval", "new-dirty", "reserve", "tail"]
-print("cycles/job: " + ", ".join(f"{n} {tot[i] / j:.0f}" for i, n in enumerate(names)) +
-      f"; new dirty per job {tot[6] / j:.2f}; write-back per job {tot[7] / j:.0f}; jobs {tot[5]}")
-print(f"new-dirty: header/runs wait + LDS copy + prefix minima {tot[11] / max(tot[6], 1):.0f} cycles per new dirty node")
-print(f"dirty-eval split: fast {tot[8] / j:.0f}, walk {tot[9] / j:.0f} (walks per job {tot[10] / j:.2f}), "
-      f"reduce {(tot[1] - tot[8] - tot[9]) / j:.0f}")
+if tot[11]:  # decider / helper commit (fit_commit_tl_mw.h)
+    apply_other = tot[8] - tot[3] - tot[4]
+    print("decider cycles/job: " + ", ".join(f"{n} {v / j:.0f}" for n, v in (
+        ("record wait", tot[0]), ("decision", tot[1]), ("exception (walks, global lists)", tot[2]),
+        ("new-dirty copy", tot[3]), ("reservation", tot[4]), ("bookkeeping", apply_other))) +
+          f"; sum {(tot[0] + tot[1] + tot[2] + tot[8]) / j:.0f}; jobs {tot[5]}")
+    print(f"new dirty per job {tot[6] / j:.2f}; jobs that walked {tot[9] / j:.3f}; "
+          f"round-end write-back {tot[7] / j:.0f} cycles/job; helpers: snapshot -> record "
+          f"{tot[10] / max(tot[11], 1):.0f} cycles over {tot[11]} records")
+else:  # single-wave commit
+    names = ["clean", "dirty-eval", "new-dirty", "reserve", "tail"]
+    print("cycles/job: " + ", ".join(f"{n} {tot[i] / j:.0f}" for i, n in enumerate(names)) +
+          f"; new dirty per job {tot[6] / j:.2f}; write-back per job {tot[7] / j:.0f}; jobs {tot[5]}")
+    print(f"new-dirty: header/runs wait + LDS copy + prefix minima {tot[11] / max(tot[6], 1):.0f} cycles per new dirty node")
+    print(f"dirty-eval split: fast {tot[8] / j:.0f}, walk {tot[9] / j:.0f} (walks per job {tot[10] / j:.2f}), "
+          f"reduce {(tot[1] - tot[8] - tot[9]) / j:.0f}")
 sc = buf[64 * 12:64 * 12 + 8]
 print(f"scan: waves {sc[4]}, nodes/wave {sc[1] / max(sc[4], 1):.0f}, cycles/node {sc[0] / max(sc[1], 1):.0f}, "
       f"long-walk batches/node {sc[2] / max(sc[1], 1):.2f}, nodes with > 4 runs {sc[3] / max(sc[1], 1):.2%}")
