@@ -104,9 +104,16 @@ def test_reload_and_invalid_requests():
             with pytest.raises(FitError):
                 adm.admit(1, 1, 10, nodes_k=9)
             # fill the cluster: 8 nodes x 64 cpus; 64-cpu jobs take whole nodes
-            got = [adm.admit(10 + i, 64, 1000)[0][0] for i in range(10)]
+            res = [adm.admit(10 + i, 64, 1000) for i in range(10)]
+            got = [r[0][0] for r in res]
             assert sum(g >= 0 for g in got) <= 8 and got[-1] == FIT_UNPLACED
-            # a fresh node table makes room again
+            # reloading Slurm's unchanged table keeps the admitted pods' reservations
+            adm.load_nodes(nodes)
+            assert adm.admit(99, 64, 1000)[0][0] == FIT_UNPLACED
+            # once Slurm counts (then frees) those jobs, a fresh table makes room again
+            for r in res:
+                if r[4]:
+                    adm.confirm(r[4])
             adm.load_nodes(nodes)
             assert adm.admit(100, 64, 1000)[0][0] >= 0
         finally:

@@ -8,7 +8,7 @@ shift
 WL=${@:-c5 c3}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_timeline_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tl_tests.txt 2>&1 || { tail -40 gpurun_out/${TAG}_tl_tests.txt; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_timeline_gpu.py tests/test_admit_gpu.py tests/test_concurrent_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tl_tests.txt 2>&1 || { tail -40 gpurun_out/${TAG}_tl_tests.txt; exit 1; }
 tail -2 gpurun_out/${TAG}_tl_tests.txt
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.txt 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.txt; exit 1; }
 tail -2 gpurun_out/${TAG}_gpu_tests.txt
