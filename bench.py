@@ -413,6 +413,21 @@ def shard_price(Engine, FIT_SHARD_NODES, parts, h_nodes, h_jobs, h_out, kmax, ms
     communicator; per round the candidate allgather + u64 min-allreduce of the bounds, host-driven
     rounds) against the default persistent engine."""
     from fitgpu import FIT_FLAG_COLLECTIVES
+    # RCCL prints its version banner on stdout when the communicator comes up: keep this process'
+    # stdout to the one JSON line (fd-level, the banner is written by the native library)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return _shard_price(Engine, FIT_SHARD_NODES, FIT_FLAG_COLLECTIVES, parts, h_nodes, h_jobs, h_out, kmax,
+                            ms_default, steps)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def _shard_price(Engine, FIT_SHARD_NODES, FIT_FLAG_COLLECTIVES, parts, h_nodes, h_jobs, h_out, kmax, ms_default,
+                 steps):
     e = Engine(device=0, shard_mode=FIT_SHARD_NODES, flags=FIT_FLAG_COLLECTIVES)
     e.load_partitions(parts)
     e.load_nodes(h_nodes)
@@ -539,7 +554,7 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
                  "oracle/fitref.c ref_place (C restatement of the scalar sequential path, every node per job)"),
                 ("component-aware", 1, m_comp, lambda s: po.cpu_place(nodes, s, parts, 1)[1],
                  "oracle/cpu_baseline.c cpu_place (own component's nodes only, vectorised scan)"),
-                ("same-algorithm", 1, m_comp, lambda s: po.cpu_place(nodes, s, parts, 1, "rounds")[1],
+                ("same-algorithm", 1, m_comp / 4, lambda s: po.cpu_place(nodes, s, parts, 1, "rounds")[1],
                  "oracle/cpu_fast.c cpu_place_rounds (the GPU's candidate-list + dirty-set rounds, 1 thread)"),
                 ("split-argmin", threads, m_split, lambda s: po.cpu_place(nodes, s, parts, threads, "split")[1],
                  f"oracle/cpu_fast.c cpu_place_split (BASELINE.md:22: each job's argmin over {threads} threads, "

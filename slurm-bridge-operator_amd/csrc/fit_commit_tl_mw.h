@@ -133,14 +133,23 @@ __device__ __forceinline__ uint64_t tm_fit0(const Seg* L, const int4* PM, int cn
 }
 
 #ifdef FIT_STAMPS
-// diagnostic build: g_tlst[comp][i] (fit_timeline.hip) — decider [0] record waits, [1] decision
-// (ring search + item merge), [2] exception path (walks, global lists), [3] new dirty copy,
-// [4] reservation + prefix minima, [5] jobs, [6] new dirty nodes, [7] round-end write-back,
-// [8] whole apply phase (copy + reservation + bookkeeping), [9] jobs that walked; helpers
-// [10] snapshot -> record cycles, [11] helper jobs
+// diagnostic build: g_tlst[comp][i] (fit_timeline.hip).  Coarse (FIT_STAMPS): [0] decider waits
+// for each round's first record, [1] decider loop cycles, [5] jobs, [6] new dirty nodes, [7]
+// round-end write-back, [8] rounds, [9] jobs that walked, [10] helper snapshot -> record cycles,
+// [11] helper records.  Fine (FIT_STAMPS_FINE, every s_memtime drains the LDS queue, so the
+// phases are inflated): [0] record waits, [1] decision (ring search + item merge), [2] exception
+// path (walks, global lists), [3] new dirty copy, [4] reservation + prefix minima, [8] whole
+// apply phase.
+#define TM_CNT(i, x) D.acc[i] += (x)
+#ifdef FIT_STAMPS_FINE
 #define TM_CLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define TM_ADD(i, x) D.acc[i] += (x)
 #else
+#define TM_CLK(v)
+#define TM_ADD(i, x)
+#endif
+#else
+#define TM_CNT(i, x)
 #define TM_CLK(v)
 #define TM_ADD(i, x)
 #endif
@@ -484,7 +493,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 // ring lists on LDS that fail at slot 0: a later start can still win only if the
                 // best so far starts later than 0 — walk them (wave-wide, one list at a time)
                 if (d.anywalk && (bm == KEY_INF || (bm >> 54) > 0)) {
-                    TM_ADD(9, 1);
+                    TM_CNT(9, 1);
                     const int32_t lim = bm == KEY_INF ? X.H : (int32_t)(bm >> 54);
                     const bool ok = live && !isg && (R.mask & jp) != 0u && jd <= X.H;
                     for (uint64_t m = __ballot(ok) & 0xffull; m; m &= m - 1) {
@@ -563,7 +572,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         mask = (uint32_t)readlane((int32_t)cur.i1.x, w);
     }
     TM_CLK(a0);
-#ifdef FIT_STAMPS
+#ifdef FIT_STAMPS_FINE
     unsigned long long a1 = a0;
 #endif
     if (placed) {
@@ -593,9 +602,9 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             }
             if (glob) D.gm |= 1ull << slot;
             D.nu += 1;
-            TM_ADD(6, 1);
+            TM_CNT(6, 1);
         }
-#ifdef FIT_STAMPS
+#ifdef FIT_STAMPS_FINE
         a1 = __builtin_amdgcn_s_memtime();
         TM_ADD(3, a1 - a0);
 #endif
@@ -657,7 +666,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
     {
         TM_CLK(a3);
         TM_ADD(8, a3 - a0);
-        TM_ADD(5, go ? 1 : 0);
+        TM_CNT(5, go ? 1 : 0);
     }
 #endif
 }
@@ -688,6 +697,9 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     int32_t oq = -1, on = -1, os = -1;
     TmRecRegs ra, rb;
     uint32_t flag = 0;
+#if defined(FIT_STAMPS) && !defined(FIT_STAMPS_FINE)
+    const unsigned long long k0 = __builtin_amdgcn_s_memtime();
+#endif
     if (P.w > 0) {
         for (unsigned sp = 0;; ++sp) {
             flag = lds_ld(&S->rec[0].h.ready);
@@ -705,6 +717,11 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     } else {
         D.exit = true;
     }
+#if defined(FIT_STAMPS) && !defined(FIT_STAMPS_FINE)
+    const unsigned long long k1 = __builtin_amdgcn_s_memtime();
+    D.acc[0] += k1 - k0;
+    D.acc[8] += 1;
+#endif
     while (!D.exit) {
         tm_decide<0>(X, D, R, ra, rb, flag, oq, on, os);
         tm_decide<1>(X, D, R, rb, ra, flag, oq, on, os);
@@ -716,6 +733,9 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
         tm_decide<7>(X, D, R, rb, ra, flag, oq, on, os);
     }
     const int t = D.t;
+#if defined(FIT_STAMPS) && !defined(FIT_STAMPS_FINE)
+    D.acc[1] += __builtin_amdgcn_s_memtime() - k1;
+#endif
     if (oq >= 0 && lane < (t & 63)) {  // the last partial group
         ((GAS int32_t*)out)[oq] = on;
         ((GAS int32_t*)outs)[oq] = os;
