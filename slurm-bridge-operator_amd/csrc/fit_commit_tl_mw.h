@@ -69,7 +69,8 @@ struct alignas(16) TmShared {
     uint32_t halt;     // decider stopped
     uint32_t fail;     // helper / decider watchdog
     int32_t res[4];    // CommitResult of the window
-    uint32_t pad[8];
+    uint32_t pubt;     // job tiles of the window published to the task ring (just in time)
+    uint32_t pad[7];
     TmRec rec[TM_R];
     Seg stage[TM_R][64];     // the run list of each record's first clean item
     TmSlot slot[TL_UCAP];
@@ -89,13 +90,45 @@ __device__ __forceinline__ T* tm_lds(T* p) {
     return (T*)(__attribute__((address_space(3))) T*)(uintptr_t)a;
 }
 
-// The tile-readiness wait of fit_commit_mw.h for this shared layout (every tile of the window is
-// published up front by the committer wave).
-__device__ __forceinline__ bool tm_tile_ready(const unsigned* tdone, unsigned need, int tt, int& ready,
-                                              TmShared* S) {
-    if (!tdone) return true;
+#ifndef TL_AHEAD
+#define TL_AHEAD 4  // job tiles published ahead of the helper that needs them (0: all up front)
+#endif
+
+// Publish the window's job tiles [pubt, upto) (uniform; lane 0 claims the range by an LDS CAS) —
+// fit_commit_mw.h mw_publish for this layout.
+__device__ __noinline__ void tm_publish(const MwTiles& T, TmShared* S, unsigned upto) {
+    const int lane = threadIdx.x & 63;
+    unsigned from = upto;
+    if (lane == 0) {
+        unsigned cur = lds_ld(&S->pubt);
+        while (cur < upto) {
+            if (__hip_atomic_compare_exchange_strong(&S->pubt, &cur, upto, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                from = cur;
+                break;
+            }
+        }
+    }
+    from = (unsigned)__builtin_amdgcn_readlane((int)from, 0);
+    if (from >= upto) return;
+    // the round's plan, bounds and tile counters were released by the committer wave before the
+    // block barrier; release again from this wave before the tasks
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    engine_publish(T.ctl, T.ring, from, upto, T.need, T.round, T.comp);
+}
+
+// The tile-readiness wait of fit_commit_mw.h for this shared layout: tiles are published just in
+// time (a helper that moves on to tile k publishes up to k + TL_AHEAD - 1 first), so a round that
+// stops early leaves at most TL_AHEAD tiles scanned for nothing, and the next round's first tile
+// is not queued behind a whole window.
+__device__ __forceinline__ bool tm_tile_ready(const MwTiles& T, int tt, int& ready, TmShared* S) {
+    if (!T.tdone) return true;
     const int tile = __builtin_amdgcn_readfirstlane(tt) / SCAN_JOBS;
     if (tile < ready) return true;
+    if (T.ring && (unsigned)tile + TL_AHEAD > lds_ld(&S->pubt))
+        tm_publish(T, S, min((unsigned)tile + TL_AHEAD, T.ntj));
+    const unsigned* tdone = T.tdone;
+    const unsigned need = T.need;
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
             break;
@@ -166,7 +199,7 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
                                        const uint64_t* __restrict__ cand_,
                                        const uint64_t* __restrict__ bnd_,
                                        const JobRec* __restrict__ wjob_, int h, int32_t H,
-                                       const unsigned* tdone, unsigned need) {
+                                       MwTiles T) {
     const GAS Seg* const slab = gview(slab_);
     const GAS TlHdr* const hdr = gview(hdr_);
     const GAS uint64_t* const cand = gview(cand_);
@@ -187,7 +220,7 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
     int ready = 0;
     auto load = [&](int tt, TmJob& o) -> bool {
         tt = min(tt, wlast) + z;
-        if (!tm_tile_ready(tdone, need, tt, ready, S)) return false;
+        if (!tm_tile_ready(T, tt, ready, S)) return false;
         o.kk = has ? cand[P.cand_off + (int64_t)tt * E + lane] : KEY_INF;
         o.J = ld_job(wjob + P.slot0 + tt);
         o.B = bnd[P.slot0 + tt];
@@ -757,7 +790,7 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
     const CompPlan& P, unsigned char* smem, Seg* __restrict__ slab, TlHdr* __restrict__ hdr,
     const uint64_t* __restrict__ cand, const uint64_t* __restrict__ bnd,
     const JobRec* __restrict__ wjob, int32_t* __restrict__ out, int32_t* __restrict__ outs,
-    int32_t H, int32_t R, const unsigned* tdone, unsigned need) {
+    int32_t H, int32_t R, MwTiles T) {
     TmShared* S = reinterpret_cast<TmShared*>(smem);
     const int32_t RS = R + TL_PAD;
     Seg* lr = reinterpret_cast<Seg*>(smem + sizeof(TmShared));
@@ -784,7 +817,7 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // placements, global-slab lists
         } else {
-            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob, wave, H, tdone, need);
+            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob, wave, H, T);
         }
     } else if (threadIdx.x == 0) {
         S->res[0] = S->res[1] = S->res[2] = S->res[3] = 0;

@@ -945,11 +945,17 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 release_agent();  // plan, bound / counter reset and the last window's run lists
-                // the whole window's tiles up front (a committer wave publishing tiles as the
-                // commit reaches them put the ring stores on the commit chain: 169.5 -> 175 ms)
-                const unsigned ntiles = ntj * (unsigned)S.nslice;
-                engine_publish(ctl, ring, 0u, ntj, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
-                target += ntiles;
+                // FIT_TL_MW: the first TL_AHEAD job tiles now, the rest by the helpers just in time
+                // (tm_tile_ready); single-wave commit: the whole window up front (a committer wave
+                // publishing tiles as the commit reaches them put the ring stores on the commit
+                // chain: 169.5 -> 175 ms)
+                const unsigned npub = (FIT_TL_MW && TL_AHEAD > 0) ? min(ntj, (unsigned)TL_AHEAD) : ntj;
+                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                if (FIT_TL_MW) {
+                    if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
+                } else {
+                    target += ntj * (unsigned)S.nslice;
+                }
                 if (f && lane == 0) atomicOr(&ctl->error, 1u);
                 if (FIT_TL_MW) {
                     acquire_agent();  // run lists written back by this block: CU-wide fresh view
@@ -965,11 +971,18 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             }
             const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
             // committed while its tiles are scanned: per-tile readiness inside
+            const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
             const CommitResult r =
                 FIT_TL_MW ? commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
-                                                &ctl->tdone[c][0], (unsigned)S.nslice)
+                                                MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
+                                                        TL_AHEAD > 0 ? ring : nullptr, ctl,
+                                                        (unsigned)rounds + 1u, (unsigned)c, ntj})
                           : commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd, wjob, perm, out,
                                                 outs, H, R, &ctl->tdone[c][0], (unsigned)S.nslice);
+            // every tile published this round (the committer's and the helpers') must be complete
+            // before the next round reuses the buffers: count them (pubt is stable after the
+            // commit's closing barrier)
+            if (FIT_TL_MW && wave == 0) target += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
             if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
             if (r.stop == 3) {
                 fail = true;
