@@ -32,7 +32,11 @@ namespace fitgpu {
 
 constexpr int TM_M = 8;   // items per record (> snapshot lag)
 constexpr int TM_R = 8;   // record ring
-constexpr int TM_H = SCAN_WAVES - 1;  // helpers
+#ifndef TL_MW_HELPERS
+#define TL_MW_HELPERS (SCAN_WAVES - 1)
+#endif
+constexpr int TM_H = TL_MW_HELPERS;  // helpers: waves 1..TM_H (the others idle during the commit)
+static_assert(TM_H >= 1 && TM_H <= SCAN_WAVES - 1, "helpers are waves 1..7");
 static_assert(TL_UCAP == 64, "one dirty slot per lane: ring / slot bit masks are 64 wide");
 static_assert(TL_KS * TL_SLICES == 64, "one candidate per helper lane");
 
@@ -816,7 +820,7 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
                 S->res[3] = r.placed;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // placements, global-slab lists
-        } else {
+        } else if (wave <= TM_H) {
             tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob, wave, H, T);
         }
     } else if (threadIdx.x == 0) {

@@ -34,6 +34,14 @@ if tot[11] and tot[4] == 0:  # decider / helper commit, coarse stamps
             print(f"  comp {c:2d} jobs {r[5]:6d} rounds {r[8]:4d} loop/job {r[1] / r[5]:6.0f} "
                   f"first-record wait/round {r[0] / max(r[8], 1):7.0f}  total {(r[0] + r[1]) / 2.4e6:6.1f} ms @2.4GHz")
 elif tot[11]:  # decider / helper commit, fine stamps (FIT_STAMPS_FINE)
+    apply_other = tot[8] - tot[3] - tot[4]
+    print("decider cycles/job: " + ", ".join(f"{n} {v / j:.0f}" for n, v in (
+        ("record wait", tot[0]), ("decision", tot[1]), ("exception (walks, global lists)", tot[2]),
+        ("new-dirty copy", tot[3]), ("reservation", tot[4]), ("bookkeeping", apply_other))) +
+          f"; sum {(tot[0] + tot[1] + tot[2] + tot[8]) / j:.0f}; jobs {tot[5]}")
+    print(f"new dirty per job {tot[6] / j:.2f}; jobs that walked {tot[9] / j:.3f}; "
+          f"round-end write-back {tot[7] / j:.0f} cycles/job; helpers: snapshot -> record "
+          f"{tot[10] / max(tot[11], 1):.0f} cycles over {tot[11]} records")
 else:  # single-wave commit
     names = ["clean", "dirty-eval", "new-dirty", "reserve", "tail"]
     print("cycles/job: " + ", ".join(f"{n} {tot[i] / j:.0f}" for i, n in enumerate(names)) +
