@@ -46,6 +46,7 @@ hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, 
 size_t engine_lds_bytes(int32_t max_component_nodes);
 size_t engine_ctl_bytes();
 size_t engine_ring_bytes();
+size_t engine_ring_tasks();
 int engine_blocks_per_cu(size_t lds);
 hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
                          const void* cs, void* co, CompPlan* plans, int ncomp, NodeRec* rec,
@@ -457,7 +458,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // (a granule overwritten before its worker read it would be lost)
     int32_t max_slices = 1;
     for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
-    if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)(engine_ring_bytes() / 8))
+    if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)engine_ring_tasks())
         return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                     nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     size_t lds = engine_lds_bytes(maxnodes);
@@ -759,7 +760,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         int32_t max_slices = 1;
         for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
         if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices >
-            (int64_t)(engine_ring_bytes() / 8))
+            (int64_t)engine_ring_tasks())
             return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                         nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     }

@@ -32,8 +32,11 @@ namespace fitgpu {
 
 constexpr int TM_M = 8;   // items per record (> snapshot lag)
 constexpr int TM_R = 8;   // record ring
+#ifndef TL_MW_SOLO
+#define TL_MW_SOLO 0  // 1: wave 4 (the decider's SIMD partner) idles; helpers are waves 1-3, 5-7
+#endif
 #ifndef TL_MW_HELPERS
-#define TL_MW_HELPERS (SCAN_WAVES - 1)
+#define TL_MW_HELPERS (SCAN_WAVES - 1 - TL_MW_SOLO)
 #endif
 constexpr int TM_H = TL_MW_HELPERS;  // helpers: waves 1..TM_H (the others idle during the commit)
 static_assert(TM_H >= 1 && TM_H <= SCAN_WAVES - 1, "helpers are waves 1..7");
@@ -167,6 +170,80 @@ __device__ __forceinline__ uint64_t tm_fit0(const Seg* L, const int4* PM, int cn
     const int4 pk = PM[min(k, R - 1)];
     fit0 = ok && pk.x >= jc && pk.y >= jm && pk.z >= jg;
     return fit0 ? tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, pos) : KEY_INF;
+}
+
+#ifndef TM_FAST
+#define TM_FAST 1  // 0: the decider's first form (4-ary ring searches, tl_reserve_lds + tl_pm_build)
+#endif
+
+typedef __attribute__((address_space(3))) v4i32 lds_v4i32;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ void lds_st4(uint32_t a, v4i32 v) { *(lds_v4i32*)(uintptr_t)a = v; }
+__device__ __forceinline__ int32_t lds_ld1(uint32_t a) {
+    return *(const __attribute__((address_space(3))) int32_t*)(uintptr_t)a;
+}
+// the previous lane's value (lane 0: `first`) / the next lane's (lane 63: `last`): DPP wave shifts
+__device__ __forceinline__ int32_t wave_shr1(int32_t v, int32_t first) {
+    return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int32_t wave_shl1(int32_t v, int32_t last) {
+    return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
+}
+
+// Reserve (jc, jm, jg) on slots [s, e) of a run list of n <= 64 runs held in registers (run
+// `lane` in g) and write the new list and its prefix minima to the LDS region L / PM — every run
+// at its new index, so a list entering the region (a new dirty node) needs no copy first, and the
+// prefix minima come from the registers (no read-back).  Same edge rules as tl_reserve_lds: the
+// runs overlapping [s, e) lose the demand, the run holding s (e) splits, the first (last) reduced
+// run merges into an equal left (right) neighbour.  The prefix minimum of a run at its new index
+// is the inclusive scan over the reduced values (a split-off piece keeps the unreduced values,
+// never below the reduced ones, so it changes no prefix after it; the head piece's own is the
+// scan before it with its values).  Lanes without a write store to `trash` (no exec branches).
+// Returns the new count, or -1 (nothing written) if it would exceed `cap`.
+__device__ __forceinline__ int tm_reserve(uint32_t L, uint32_t PM, uint32_t trash, const Seg& g, int n,
+                                          int cap, int32_t s, int32_t e, int32_t jc, int32_t jm,
+                                          int32_t jg) {
+    const int lane = threadIdx.x & 63;
+    // every cross-lane value first (DPP reads with the full wave active), then only selects
+    const int32_t a = wave_shr1(g.end, 0);  // the run's start
+    const int32_t lc = wave_shr1(g.cpu, 0), lm = wave_shr1(g.mem, 0), lg = wave_shr1(g.gpu, 0);
+    const int32_t nc = wave_shl1(g.cpu, 0), nm = wave_shl1(g.mem, 0), ng = wave_shl1(g.gpu, 0);
+    const bool v = lane < n;
+    const int32_t rc = g.cpu - jc, rm = g.mem - jm, rg = g.gpu - jg;
+    const uint64_t mov = __ballot(v & (a < e) & (g.end > s));
+    const uint64_t mh = __ballot(v & (a < s)), mt = __ballot(v & (g.end > e));
+    const uint64_t meqL = __ballot((lc == rc) & (lm == rm) & (lg == rg));
+    const uint64_t meqR = __ballot((nc == rc) & (nm == rm) & (ng == rg));
+    const int i0 = __builtin_ctzll(mov), i1 = 63 - __builtin_clzll(mov);
+    const int head = (int)((mh >> i0) & 1ull), tail = (int)((mt >> i1) & 1ull);
+    const int mergeL = (int)((meqL >> i0) & 1ull) & (head ^ 1) & (int)(i0 > 0);
+    const int mergeR = (int)((meqR >> i1) & 1ull) & (tail ^ 1) & (int)(i1 < n - 1);
+    const int nn = n + head + tail - mergeL - mergeR;
+    if (nn > cap) return -1;
+    const int sh = head - mergeL;                  // index shift of the reduced runs
+    const int st = head + tail - mergeL - mergeR;  // index shift of the runs after them
+    const bool inr = (lane >= i0) & (lane <= i1);
+    const Seg u{inr ? min(g.end, e) : g.end, inr ? rc : g.cpu, inr ? rm : g.mem, inr ? rg : g.gpu};
+    const int32_t pc = wave_scan_min(v ? u.cpu : TL_BIG), pm = wave_scan_min(v ? u.mem : TL_BIG),
+                  pg = wave_scan_min(v ? u.gpu : TL_BIG);
+    const int32_t xc = wave_shr1(pc, TL_BIG), xm = wave_shr1(pm, TL_BIG), xg = wave_shr1(pg, TL_BIG);
+    // every run at its new index (the two a merge drops excluded)
+    const int dest = lane + (lane < i0 ? 0 : (lane > i1 ? st : sh));
+    const bool wp = v & !((mergeL != 0) & (lane == i0 - 1)) & !((mergeR != 0) & (lane == i1));
+    const uint32_t od = 16u * (uint32_t)dest;
+    lds_st4(wp ? L + od : trash, v4i32{u.end, u.cpu, u.mem, u.gpu});
+    lds_st4(wp ? PM + od : trash, v4i32{pc, pm, pg, 0});
+    // the head piece (lane i0): [a, s) unreduced at i0, its prefix minima the scan before it
+    const bool wh = (head != 0) & (lane == i0);
+    const uint32_t oh = 16u * (uint32_t)i0;
+    lds_st4(wh ? L + oh : trash, v4i32{s, g.cpu, g.mem, g.gpu});
+    lds_st4(wh ? PM + oh : trash, v4i32{min(xc, g.cpu), min(xm, g.mem), min(xg, g.gpu), 0});
+    // the tail piece (lane i1): [e, end) unreduced after the reduced runs
+    const bool wt = (tail != 0) & (lane == i1);
+    const uint32_t ot = 16u * (uint32_t)(i1 + sh + 1);
+    lds_st4(wt ? L + ot : trash, v4i32{g.end, g.cpu, g.mem, g.gpu});
+    lds_st4(wt ? PM + ot : trash, v4i32{pc, pm, pg, 0});
+    return nn;
 }
 
 #ifdef FIT_STAMPS
@@ -375,6 +452,7 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
 // ------------------------------------------------------------------------------ decider
 struct TmRing {  // lanes 0..7: job t's decision in lane t & 7
     int32_t slot;   // dirty slot
+    int32_t ro;     // its LDS region's first run (slot * RS)
     uint32_t pos;   // node position
     uint32_t mask;
     int32_t cnt;    // its list's run count after that decision
@@ -414,6 +492,7 @@ struct TmCtx {  // the decider's window constants (SGPRs)
 struct TmDec {
     int t, nu, placed, stop;
     uint64_t gm;  // dirty slots whose list lives in the global slab
+    uint32_t rb[TM_R];  // LDS byte address of ring entry i's run-list region (uniform)
     bool exit;
 #ifdef FIT_STAMPS
     unsigned long long acc[10];
@@ -463,8 +542,30 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         const bool ok = live && (R.mask & jp) != 0u && jd <= X.H;
         bool fit0 = false;
         const int sl = R.slot < 0 ? 0 : R.slot;
+#if TM_FAST
+        // ring list i's first run ending at or after jd: run `lane` of all 8 lists (one round
+        // trip), a ballot each (a list ends at H >= jd, so the first set bit is a real run), then
+        // lane i reads list i's prefix minima there
+        uint64_t rk;
+        {
+            const uint32_t lo = 16u * (uint32_t)min(lane, X.R - 1);
+            int32_t ev[TM_R];
+#pragma unroll
+            for (int i = 0; i < TM_R; ++i) ev[i] = lds_ld1(D.rb[i] + lo);
+            int32_t kk = 0;
+#pragma unroll
+            for (int i = 0; i < TM_R; ++i) {
+                const uint64_t m = __ballot(ev[i] >= jd);
+                kk = writelane(m ? (int)__builtin_ctzll(m) : 0, i, kk);
+            }
+            const int4 pk = X.pmr[R.ro + min(kk, X.R - 1)];
+            fit0 = ok && !isg && pk.x >= jc && pk.y >= jm && pk.z >= jg;
+            rk = fit0 ? tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, R.pos) : KEY_INF;
+        }
+#else
         const uint64_t rk = tm_fit0(X.lr + sl * X.RS, X.pmr + sl * X.RS, R.cnt, X.R, ok && !isg, jc, jm,
                                     jg, jd, R.pos, fit0);
+#endif
         d.anywalk = __ballot(ok && !fit0) != 0ull;
         // item staleness: its node is in the live ring (lanes 8..15 hold a copy of the ring, so
         // row_ror:k, k = 0..7, shows lane i < 8 every ring entry once)
@@ -616,14 +717,70 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         Seg* const L = X.lr + slot * X.RS;
         int4* const PM = X.pmr + slot * X.RS;
         bool glob = (D.gm >> slot) & 1ull;
+#if TM_FAST
+        // the list in registers (run `lane`): a new dirty node's from the helper's stage (or the
+        // slab), an LDS list's from its region; tm_reserve writes the whole new list
+        Seg g{0, 0, 0, 0};
+        if (fresh) {  // a clean winner becomes dirty slot nu
+            glob = cnt > X.R;
+            if (!glob) {
+                // typed loads on both sides: a plain select of the two pointers becomes one flat
+                // load, which waits on the vector-memory path even for the LDS stage
+                if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {  // staged by the helper
+                    const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
+                    g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
+                } else {  // not the record's first clean item (that one was written meanwhile)
+                    const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
+                    g = Seg{x.x, x.y, x.z, x.w};
+                }
+            }
+            if (lane == 0) {
+                const uint32_t rel = pos - X.nb;
+                X.bitmap[rel >> 5] |= 1u << (rel & 31);
+                S->slot[slot] = TmSlot{pos, mask, orig, cnt, readlane((int32_t)cur.i1.z, w),
+                                       readlane((int32_t)cur.i1.w, w), readlane((int32_t)cur.i2.x, w),
+                                       glob ? 1 : 0};
+            }
+            if (glob) D.gm |= 1ull << slot;
+            D.nu += 1;
+            TM_CNT(6, 1);
+        } else if (!glob) {
+            const v4u32 x = lds4(L + min(lane, X.R - 1))[0];
+            g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
+        }
+#ifdef FIT_STAMPS_FINE
+        a1 = __builtin_amdgcn_s_memtime();
+        TM_ADD(3, a1 - a0);
+#endif
+        int nn;
+        if (!glob) {
+            nn = tm_reserve(lds_addr(L), lds_addr(PM), lds_addr(&S->scr[lane]), g, cnt, X.R, start,
+                            start + jd, jc, jm, jg);
+            if (nn < 0) {  // outgrows its LDS region: the list moves to the global slab
+                Seg* gl = X.slab + (int64_t)pos * TL_MAX_SLOTS;
+                if (!fresh && lane < cnt) gl[lane] = g;  // a new dirty node's list is there already
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                nn = tl_reserve_any(gl, cnt, start, start + jd, jc, jm, jg, S->scr);
+                D.gm |= 1ull << slot;
+                glob = true;
+            }
+        } else {
+            nn = tl_reserve_any(X.slab + (int64_t)pos * TL_MAX_SLOTS, cnt, start, start + jd, jc, jm, jg,
+                                S->scr);
+        }
+#else
         if (fresh) {  // a clean winner becomes dirty slot nu: its runs into the slot's LDS region
             glob = cnt > X.R;
             if (!glob) {
+                // typed loads on both sides: a plain select of the two pointers becomes one flat
+                // load, which waits on the vector-memory path even for the LDS stage
                 Seg g;
-                if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {
-                    g = S->stage[t & (TM_R - 1)][lane];  // staged by the helper
+                if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {  // staged by the helper
+                    const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
+                    g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
                 } else {  // not the record's first clean item (that one was written meanwhile)
-                    g = X.slab[(int64_t)pos * TL_MAX_SLOTS + lane];
+                    const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
+                    g = Seg{x.x, x.y, x.z, x.w};
                 }
                 if (lane < cnt) L[lane] = g;
                 const Seg p = lane < cnt ? g : Seg{0, TL_BIG, TL_BIG, TL_BIG};
@@ -662,6 +819,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             nn = tl_reserve_any(X.slab + (int64_t)pos * TL_MAX_SLOTS, cnt, start, start + jd, jc, jm, jg,
                                 S->scr);
         }
+#endif
         if (lane == 0) {  // the helpers' view of the slot
             S->slot[slot].cnt = nn;
             S->slot[slot].glob = glob ? 1 : 0;
@@ -674,6 +832,8 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         // ring: an older entry of the same slot dies; lane E takes job t
         R.job = (R.slot == slot) ? -1 : R.job;
         R.slot = writelane_c<E>(slot, R.slot);
+        D.rb[E] = (uint32_t)rfl((int32_t)lds_addr(L));
+        R.ro = writelane_c<E>(slot * X.RS, R.ro);
         R.pos = (uint32_t)writelane_c<E>((int32_t)pos, (int32_t)R.pos);
         R.mask = (uint32_t)writelane_c<E>((int32_t)mask, (int32_t)R.mask);
         R.cnt = writelane_c<E>(cnt, R.cnt);
@@ -730,7 +890,8 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     __builtin_amdgcn_s_setprio(3);  // shares its SIMD with a helper wave
     TmDec D{};
     D.exit = false;
-    TmRing R{-1, 0xffffffffu, 0u, 0, -1, -1};
+    for (int i = 0; i < TM_R; ++i) D.rb[i] = lds_addr(X.lr);
+    TmRing R{-1, 0, 0xffffffffu, 0u, 0, -1, -1};
     int32_t oq = -1, on = -1, os = -1;
     TmRecRegs ra, rb;
     uint32_t flag = 0;
@@ -820,8 +981,9 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
                 S->res[3] = r.placed;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // placements, global-slab lists
-        } else if (wave <= TM_H) {
-            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob, wave, H, T);
+        } else if (TL_MW_SOLO ? wave != 4 : wave <= TM_H) {
+            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob,
+                      TL_MW_SOLO && wave > 4 ? wave - 1 : wave, H, T);
         }
     } else if (threadIdx.x == 0) {
         S->res[0] = S->res[1] = S->res[2] = S->res[3] = 0;

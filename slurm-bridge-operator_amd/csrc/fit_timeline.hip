@@ -878,6 +878,9 @@ __global__ __launch_bounds__(64) void k_commit_tl(
     if (threadIdx.x == 0) res[c] = r;
 }
 
+#ifndef TL_PRIO
+#define TL_PRIO 0  // 1: each round's first job tile through the priority ring (fit_engine_ctl.h)
+#endif
 #ifndef FIT_TL_MW
 #define FIT_TL_MW 1  // 0: the single-wave committer (commit_tl_window) in k_engine_tl too
 #endif
@@ -950,7 +953,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 // publishing tiles as the commit reaches them put the ring stores on the commit
                 // chain: 169.5 -> 175 ms)
                 const unsigned npub = (FIT_TL_MW && TL_AHEAD > 0) ? min(ntj, (unsigned)TL_AHEAD) : ntj;
-                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                // TL_PRIO: the first tile through the priority ring (the commit waits for it; the
+                // task ring holds other components' tiles published ahead of their need)
+                const unsigned np0 = (TL_PRIO && npub > 0) ? 1u : 0u;
+                if (np0) engine_publish_prio(ctl, ring, 0u, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                engine_publish(ctl, ring, np0, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
                 if (FIT_TL_MW) {
                     if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
                 } else {
@@ -1020,10 +1027,14 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64);
     int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
     int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
+    unsigned idx = 0;     // thread 0: the task-ring index claimed and not yet served
+    bool held = false;
     for (;;) {
         if (threadIdx.x == 0) {
-            const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (!held) {
+                idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                held = true;
+            }
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
             unsigned long long task = TASK_EXIT;
             for (unsigned spins = 0;; ++spins) {
@@ -1032,7 +1043,33 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                                                                __HIP_MEMORY_SCOPE_AGENT);
                 if ((g >> 32) == want) {
                     task = g;
+                    held = false;
                     break;
+                }
+                // TL_PRIO: while its own tile is not yet published, an idle worker takes a
+                // round's first tile from the priority ring (the claimed index stays held)
+                if (TL_PRIO) {
+                    unsigned ph = ld_agent(&ctl->p_head);
+                    if (ph < ld_agent(&ctl->p_tail)) {
+                        if (__hip_atomic_compare_exchange_strong(&ctl->p_head, &ph, ph + 1u, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            const unsigned long long pw = (unsigned long long)(ph / PCAP + 1);
+                            for (unsigned ps = 0;; ++ps) {  // reserved before stored: a short wait
+                                const unsigned long long pg = __hip_atomic_load(
+                                    ring + QCAP + (ph & (PCAP - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                if ((pg >> 32) == pw) {
+                                    task = pg;
+                                    break;
+                                }
+                                if (ps > SPIN_LIMIT) {
+                                    atomicOr(&ctl->error, 1u);
+                                    break;
+                                }
+                            }
+                            break;
+                        }
+                        continue;  // another worker took it: look again
+                    }
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
                 if (spins > SPIN_LIMIT) {

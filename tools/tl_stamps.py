@@ -6,7 +6,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "slurm-bridge-operator_amd")]
 from fitgpu import _lib  # noqa: E402
-_lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", "libfitgpu_stamps.so")
+_lib.LIB_PATH = os.environ.get("FITGPU_STAMPS_LIB") or os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", "libfitgpu_stamps.so")
 from fitgpu import Engine, synth  # noqa: E402
 
 nn = int(sys.argv[1]) if len(sys.argv) > 1 else None
