@@ -731,7 +731,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
                                         "timeline engine's LDS", maxnodes);
     const int64_t wcap = std::min(c->wmax, 8192);
     int slices = TL_SLICES, tl_min_sub = TL_MIN_SUB;
-    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), 64 / TL_KS));
+    if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), TL_SLICES));
     if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
     const int64_t per_comp_cand = wcap * slices * TL_KS;
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||

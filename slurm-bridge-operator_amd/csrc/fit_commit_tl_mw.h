@@ -41,7 +41,9 @@ constexpr int TM_R = 8;   // record ring
 constexpr int TM_H = TL_MW_HELPERS;  // helpers: waves 1..TM_H (the others idle during the commit)
 static_assert(TM_H >= 1 && TM_H <= SCAN_WAVES - 1, "helpers are waves 1..7");
 static_assert(TL_UCAP == 64, "one dirty slot per lane: ring / slot bit masks are 64 wide");
-static_assert(TL_KS * TL_SLICES == 64, "one candidate per helper lane");
+constexpr int TM_CPL = TL_KS * TL_SLICES / 64;  // clean candidates per helper lane
+static_assert(TM_CPL * 64 == TL_KS * TL_SLICES && TM_CPL >= 1 && TM_CPL <= 2,
+              "64 or 128 candidates per job (one or two per helper lane)");
 
 struct alignas(16) TmItem {  // 48 B
     uint32_t klo, khi;       // key = start << 54 | score << 22 | position
@@ -270,7 +272,7 @@ __device__ __forceinline__ int tm_reserve(uint32_t L, uint32_t PM, uint32_t tras
 
 // ------------------------------------------------------------------------------- helper
 struct TmJob {
-    uint64_t kk, B;
+    uint64_t kk[TM_CPL], B;
     JobRec J;
 };
 
@@ -292,8 +294,7 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
     int4* const pmr = tm_lds(pmr_);
     uint32_t* const bitmap = tm_lds(bitmap_);
     const int lane = threadIdx.x & 63;
-    const int E = P.nslice * TL_KS;  // 64 candidates per job (one per lane)
-    const bool has = lane < E;
+    const int E = P.nslice * TL_KS;  // candidates per job (lane + 64 c, c < TM_CPL)
     const int wlast = P.w - 1;
     const int z = opaque_zero();
     const uint32_t nb = (uint32_t)P.nb;
@@ -302,7 +303,9 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
     auto load = [&](int tt, TmJob& o) -> bool {
         tt = min(tt, wlast) + z;
         if (!tm_tile_ready(T, tt, ready, S)) return false;
-        o.kk = has ? cand[P.cand_off + (int64_t)tt * E + lane] : KEY_INF;
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c)
+            o.kk[c] = lane + 64 * c < E ? cand[P.cand_off + (int64_t)tt * E + lane + 64 * c] : KEY_INF;
         o.J = ld_job(wjob + P.slot0 + tt);
         o.B = bnd[P.slot0 + tt];
         return true;
@@ -348,14 +351,15 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         const uint64_t B = cur.B;
         const int32_t jc = rfl(J.cpu), jm = rfl(J.mem), jg = rfl(J.gpu), jd = rfl(J.wall);
         const uint32_t jp = (uint32_t)rfl((int)J.pbit);
-        // clean candidate of this lane
-        uint64_t x0 = KEY_INF;
-        {
-            const uint64_t k = cur.kk;
+        // clean candidates of this lane
+        uint64_t xc[TM_CPL];
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c) {
+            const uint64_t k = cur.kk[c];
             const bool ok = k <= B && k != KEY_INF;
             const uint32_t rel = ok ? ((uint32_t)k & TL_POS_MASK) - nb : 0u;
             const bool dirty = (bitmap[rel >> 5] >> (rel & 31)) & 1u;
-            x0 = ok && !dirty ? k : KEY_INF;
+            xc[c] = ok && !dirty ? k : KEY_INF;
         }
         // dirty slot of this lane (slot = lane < nu), LDS lists only
         const TmSlot si = S->slot[lane < nu ? lane : 0];
@@ -374,59 +378,103 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         }
         xd = xd <= B ? xd : KEY_INF;
         // extraction: the nmax smallest entries, one wave minimum (two 32-bit passes) each; every
-        // entry remembers which item it became (sel: 4 bits per entry)
+        // entry remembers which item it became (sel: 4 bits per entry; entries 0..TM_CPL-1 clean,
+        // TM_CPL dirty), the lane's entries sorted once so each lane offers its smallest
         const int nmax = min(TM_M, t - v + 1);
-        uint64_t q0 = umin64(x0, xd), q1 = umax64(x0, xd);
-        int o0 = x0 < xd ? 0 : 1, o1 = 1 - o0;  // entry of q0 / q1 (0 clean, 1 dirty)
+        constexpr int NE = TM_CPL + 1;
+        uint64_t q[NE];
+        int o[NE];
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c) {
+            q[c] = xc[c];
+            o[c] = c;
+        }
+        q[TM_CPL] = xd;
+        o[TM_CPL] = TM_CPL;
+        auto cswap = [&](int i, int j) {
+            const bool sw = q[j] < q[i];
+            const uint64_t qi = q[i], qj = q[j];
+            const int oi = o[i], oj = o[j];
+            q[i] = sw ? qj : qi;
+            q[j] = sw ? qi : qj;
+            o[i] = sw ? oj : oi;
+            o[j] = sw ? oi : oj;
+        };
+        if constexpr (NE == 2) {
+            cswap(0, 1);
+        } else {
+            cswap(0, 1);
+            cswap(1, 2);
+            cswap(0, 1);
+        }
         uint32_t sel = 0u;
         int n = 0;
-        uint64_t myitem = KEY_INF;  // item `lane` (lanes < 8)
 #pragma unroll
         for (int i = 0; i < TM_M; ++i) {
-            const uint32_t hh = (uint32_t)(q0 >> 32), ll = (uint32_t)q0;
+            const uint32_t hh = (uint32_t)(q[0] >> 32), ll = (uint32_t)q[0];
             const uint32_t mh = wave_min32_all(hh);
             const uint32_t ml = wave_min32_all(hh == mh ? ll : 0xffffffffu);
             const bool take = i < nmax && (mh & ml) != 0xffffffffu;
             const bool me = take && hh == mh && ll == ml;  // keys of distinct nodes are unique
             n += take ? 1 : 0;
-            if (lane == i) myitem = take ? (((uint64_t)mh << 32) | ml) : KEY_INF;
-            sel = me ? sel | ((uint32_t)(i + 1) << (4 * o0)) : sel;
-            q0 = me ? q1 : q0;
-            o0 = me ? o1 : o0;
-            q1 = me ? KEY_INF : q1;
+            sel = me ? sel | ((uint32_t)(i + 1) << (4 * o[0])) : sel;
+#pragma unroll
+            for (int e = 0; e + 1 < NE; ++e) {
+                q[e] = me ? q[e + 1] : q[e];
+                o[e] = me ? o[e + 1] : o[e];
+            }
+            q[NE - 1] = me ? KEY_INF : q[NE - 1];
         }
         n = rfl(n);
         // clean items need their node's header fields; the first clean item's run list is staged
-        const uint32_t ix0 = sel & 15u, ix1 = (sel >> 4) & 15u;
-        const bool cl = ix0 != 0u;
-        const uint32_t cpos = cl ? ((uint32_t)x0 & TL_POS_MASK) : nb;
-        const uint32_t first = wave_min32_all(cl ? ix0 : 15u);
-        const uint64_t fm = __ballot(cl && ix0 == first);
-        const uint32_t spos = fm ? (uint32_t)readlane((int32_t)cpos, __builtin_ctzll(fm)) : 0xffffffffu;
-        TlHdr ch;
-        {
-            const GAS v4i32* hp = (const GAS v4i32*)(hdr + cpos);
+        uint32_t ixc[TM_CPL], cpos[TM_CPL];
+        uint32_t fmin = 15u;
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c) {
+            ixc[c] = (sel >> (4 * c)) & 15u;
+            cpos[c] = ixc[c] ? ((uint32_t)xc[c] & TL_POS_MASK) : nb;
+            fmin = min(fmin, ixc[c] ? ixc[c] : 15u);
+        }
+        const uint32_t ix1 = (sel >> (4 * TM_CPL)) & 15u;
+        const uint32_t first = wave_min32_all(fmin);
+        uint32_t spos = 0xffffffffu;
+        int fl = 0, fc = 0;
+#pragma unroll
+        for (int c = TM_CPL - 1; c >= 0; --c) {
+            const uint64_t fm = __ballot(ixc[c] != 0u && ixc[c] == first);
+            if (fm) {
+                fl = __builtin_ctzll(fm);
+                fc = c;
+                spos = (uint32_t)readlane((int32_t)cpos[c], fl);
+            }
+        }
+        TlHdr ch[TM_CPL];
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c) {
+            const GAS v4i32* hp = (const GAS v4i32*)(hdr + cpos[c]);
             const v4i32 a = hp[0], b = hp[1];
-            ch.cnt = a.x;
-            ch.cpu = a.y;
-            ch.mem = a.z;
-            ch.gpu = a.w;
-            ch.mask = (uint32_t)b.x;
-            ch.orig = b.y;
+            ch[c].cnt = a.x;
+            ch[c].cpu = a.y;
+            ch[c].mem = a.z;
+            ch[c].gpu = a.w;
+            ch[c].mask = (uint32_t)b.x;
+            ch[c].orig = b.y;
         }
         const v4i32 sv = *(const GAS v4i32*)(slab + (int64_t)(spos != 0xffffffffu ? spos : nb) * TL_MAX_SLOTS + lane);
         const Seg srun{sv.x, sv.y, sv.z, sv.w};
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next job's prefetch too (older)
         TmRec* const Rr = &S->rec[t & (TM_R - 1)];
-        if (cl)
-            Rr->it[ix0 - 1u] = TmItem{(uint32_t)x0, (uint32_t)(x0 >> 32), -1, ch.orig, ch.mask, ch.cnt,
-                                      ch.cpu, ch.mem, ch.gpu, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c)
+            if (ixc[c])
+                Rr->it[ixc[c] - 1u] = TmItem{(uint32_t)xc[c], (uint32_t)(xc[c] >> 32), -1, ch[c].orig,
+                                             ch[c].mask, ch[c].cnt, ch[c].cpu, ch[c].mem, ch[c].gpu, 0, 0, 0};
         if (ix1)
             Rr->it[ix1 - 1u] = TmItem{(uint32_t)xd, (uint32_t)(xd >> 32), lane, si.orig, si.mask, si.cnt,
                                       si.cc, si.cm, si.cg, 0, 0, 0};
         int32_t scnt = 0;
         if (spos != 0xffffffffu) {
-            scnt = readlane(ch.cnt, __builtin_ctzll(fm));
+            scnt = readlane(fc == 0 ? ch[0].cnt : ch[TM_CPL - 1].cnt, fl);
             if (scnt <= R && lane < scnt) S->stage[t & (TM_R - 1)][lane] = srun;
         }
         if (lane == 0) {
@@ -443,7 +491,6 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         hs_acc += __builtin_amdgcn_s_memtime() - hs0;
         ++hs_n;
 #endif
-        (void)myitem;
         cur = nxt;
         t += TM_H;
     }
@@ -519,10 +566,6 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
     const int lane = threadIdx.x & 63;
     const int t = D.t;
     if (t >= X.w) D.exit = true;
-    // publish the decisions so far: release store of {decided, nu}
-    lds_release();
-    __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_WORKGROUP);
     const TmRec* Rn = &S->rec[(E + 1) & (TM_R - 1)];  // t == E (mod 8) while the window runs
     const uint32_t flag_n = lds_ld(&Rn->h.ready);
 
@@ -843,7 +886,13 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
     } else if (go) {
         R.job = writelane_c<E>(-1, R.job);  // nothing written by job t
     }
-    // read record t+1's data after acquiring its ready word (the load above is long done)
+    // publish the decisions so far (release store of {decided, nu}: the reservation's list and
+    // prefix-minimum writes before it), then read record t+1's data after acquiring its ready
+    // word (the load above is long done) — at the end of the step, so the next step starts
+    // without draining the LDS queue and the record reads overlap the parking below
+    lds_release();
+    __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)(t + (go ? 1 : 0)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     flag = flag_n;
     lds_acquire();
     tm_read_rec(Rn, lane & 7, nxt);

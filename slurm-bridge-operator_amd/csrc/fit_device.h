@@ -90,7 +90,12 @@ constexpr int TL_MAX_SLOTS = 1024;  // horizon limit (slots); the C5 horizon
 #define TL_UCAP_DEF 64
 #endif
 constexpr int TL_UCAP = TL_UCAP_DEF;  // dirty nodes per component per round (TL_UCAP / 64 per lane)
-constexpr int TL_SLICES = 64 / TL_KS;  // block-slices per job (over all ranks) in the timeline scan
+#ifndef FIT_TL_CAND
+#define FIT_TL_CAND 128
+#endif
+constexpr int TL_CAND = FIT_TL_CAND;  // candidates per job of the timeline scan (64 or 128)
+static_assert((TL_CAND == 64 || TL_CAND == 128) && TL_CAND % TL_KS == 0, "FIT_TL_CAND: 64 or 128");
+constexpr int TL_SLICES = TL_CAND / TL_KS;  // block-slices per job (over all ranks) in the timeline scan
 constexpr int TL_MIN_SUB = 32;      // minimum nodes per wave sub-slice in the timeline scan
 constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position
 constexpr uint32_t TL_POS_MASK = (1u << TL_POS_BITS) - 1u;

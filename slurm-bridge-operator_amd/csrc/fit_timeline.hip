@@ -66,9 +66,41 @@ struct TlWalk {
 
 // One run: extend / break the feasible stretch; a stretch of d slots gives the key.  A lane
 // stops once every start it could still find is later than `lim` (the start of its cut key).
+#ifndef TL_STEP_BF
+#define TL_STEP_BF 1  // 0: the branchy form below (same walk)
+#endif
+// tl_step on lanes where `vld` holds (a lane's runs past its list's end: vld false, and it stays
+// false for the rest of the walk, so only the key and liveness need the gate)
+__device__ __forceinline__ void tl_step_v(TlWalk& w, bool vld, int32_t end, int32_t c, int32_t m,
+                                          int32_t g, int32_t jc, int32_t jm, int32_t jg, int32_t d,
+                                          int32_t H, int32_t lim, uint32_t pos) {
+    const bool f = (c >= jc) & (m >= jm) & (g >= jg);
+    const bool nw = w.ra < 0;
+    const int32_t ra = f ? (nw ? w.a : w.ra) : -1;
+    const int32_t mc = nw ? c : min(w.mc, c), mm = nw ? m : min(w.mm, m), mg = nw ? g : min(w.mg, g);
+    const bool done = f & (end - ra >= d);
+    const bool kill = f ? (ra > lim) : ((end + d > H) | (end > lim));
+    const uint64_t k = tl_key(ra, mc, mm, mg, jc, jm, jg, pos);
+    const bool lv = w.live & vld;
+    w.key = (lv & done) ? k : w.key;
+    w.live = vld ? (w.live & !done & !kill) : w.live;
+    w.ra = ra;
+    w.mc = mc;
+    w.mm = mm;
+    w.mg = mg;
+    w.a = end;
+}
+
 __device__ __forceinline__ void tl_step(TlWalk& w, int32_t end, int32_t c, int32_t m, int32_t g,
                                         int32_t jc, int32_t jm, int32_t jg, int32_t d, int32_t H,
                                         int32_t lim, uint32_t pos) {
+#if TL_STEP_BF
+    // straight-line form: every lane computes the step, only a live lane's key / liveness change
+    // (a finished lane's stretch fields are never read again), so lanes that diverge on "fits"
+    // cost no exec-mask branches
+    tl_step_v(w, true, end, c, m, g, jc, jm, jg, d, H, lim, pos);
+    return;
+#endif
     if (!w.live) return;
     if (c >= jc && m >= jm && g >= jg) {
         if (w.ra < 0) {
@@ -124,8 +156,13 @@ __device__ __forceinline__ uint64_t tl_eval4(const Seg* sg, int cnt, int cap, bo
 #pragma unroll
         for (int u = 0; u < 4; ++u) g[u] = sg[min(i + u, cap - 1)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u) {
+#if TL_STEP_BF
+            tl_step_v(w, i + u < cnt, g[u].end, g[u].cpu, g[u].mem, g[u].gpu, jc, jm, jg, d, H, lim, pos);
+#else
             if (i + u < cnt) tl_step(w, g[u].end, g[u].cpu, g[u].mem, g[u].gpu, jc, jm, jg, d, H, lim, pos);
+#endif
+        }
     }
     return w.key;
 }
@@ -984,7 +1021,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                                                 MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
                                                         TL_AHEAD > 0 ? ring : nullptr, ctl,
                                                         (unsigned)rounds + 1u, (unsigned)c, ntj})
-                          : commit_tl_window<1>(P, c, smem, slab, hdr, cand, 0, 1, bnd, wjob, perm, out,
+                          : commit_tl_window<TL_CAND / 64>(P, c, smem, slab, hdr, cand, 0, 1, bnd, wjob, perm, out,
                                                 outs, H, R, &ctl->tdone[c][0], (unsigned)S.nslice);
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
