@@ -84,10 +84,11 @@ struct alignas(16) MwItem {  // 48 B; the decider reads the first 36
 };
 
 struct alignas(16) MwHdr {
-    uint32_t ready;  // t + 1 once the record of job t is complete (release store, last)
+    uint32_t ready;  // i + 1 once record i is complete (release store, last)
     int32_t v, n, q;
     int32_t cpu, mem, gpu, wall;
-    uint32_t pbit, pad;
+    uint32_t pbit;
+    int32_t tj;      // the record's job (window index); P.w: the window has no live job left
     uint64_t B;
 };
 
@@ -159,6 +160,9 @@ struct MwTiles {
     unsigned round;  // task round tag
     unsigned comp;
     unsigned ntj;    // job tiles of the window
+    // per job tile: jobs with a node that fits them at the round's start (k_engine's scan ORs
+    // them in before it counts the tile done); nullptr: every job of the window is live
+    const unsigned long long* feas;
 };
 #ifndef ENGINE_AHEAD
 #define ENGINE_AHEAD 4  // 0: every tile of the window published up front
@@ -416,6 +420,79 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
     return true;
 }
 
+// ---------------------------------------------------------------------------- live jobs
+// A job with no node that fits it at the round's start state is unplaced whatever the jobs
+// before it take (node state only shrinks within a placement) and changes nothing: the commit
+// skips it (its output is already FIT_UNPLACED from k_prefilter).  The decider then walks the
+// LIVE jobs only: record i (ring lane i & 7, snapshot counts, ready word) belongs to the i-th
+// live job of the window, whose window index the record's header carries; a record whose job
+// index is the window size ends the window.  C3: ~14 % of a component's jobs (the ones nothing
+// fits once the cluster has filled) no longer cost a decider step.
+#ifndef FIT_SKIP_CERT
+#define FIT_SKIP_CERT 1  // 0: every job of the window is live (A/B knob)
+#endif
+struct MwCursor {
+    int ct;       // job tile of the cursor
+    uint64_t cm;  // live jobs of tile ct not yet taken
+};
+// move the cursor to the next job tile (uniform): its live-job mask once the tile is complete;
+// false: halted / watchdog.  Past the window's last tile the mask stays empty.
+__device__ __forceinline__ bool mw_cursor_tile(const MwTiles& T, const CompPlan& P, MwCursor& C,
+                                               int& ready, MwShared* S) {
+    if ((C.ct + 1) * SCAN_JOBS >= P.w) {
+        C.cm = 0ull;
+        return true;
+    }
+    ++C.ct;
+    const int n = min(SCAN_JOBS, P.w - C.ct * SCAN_JOBS);
+    const uint64_t valid = n >= 64 ? ~0ull : (1ull << n) - 1ull;
+    if (FIT_SKIP_CERT && T.feas) {
+        if (!mw_tile_ready(T, C.ct * SCAN_JOBS, ready, S)) return false;
+        const uint64_t f = __hip_atomic_load(gview(T.feas) + C.ct, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)f);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(f >> 32));
+        C.cm = (((uint64_t)hi << 32) | lo) & valid;
+    } else {
+        C.cm = valid;
+    }
+    return true;
+}
+// the k-th next live job (1 <= k <= 64, window index; P.w once the window has none left)
+__device__ __forceinline__ bool mw_skip_live(const MwTiles& T, const CompPlan& P, MwCursor& C,
+                                             int& ready, MwShared* S, int k, int& tj) {
+    for (;;) {  // uniform; a tile holds ~7 records of each helper, so this rarely loops
+        const int pc = __builtin_popcountll(C.cm);
+        if (pc >= k) break;
+        if ((C.ct + 1) * SCAN_JOBS >= P.w) {
+            C.cm = 0ull;
+            tj = P.w;
+            return true;
+        }
+        k -= pc;
+        if (!mw_cursor_tile(T, P, C, ready, S)) return false;
+    }
+    for (int j = 1; j < k; ++j) C.cm &= C.cm - 1ull;
+    tj = C.ct * SCAN_JOBS + (int)__builtin_ctzll(C.cm);
+    C.cm &= C.cm - 1ull;
+    return true;
+}
+
+// The tile hand-off copied into SGPRs: mw_helper receives it in private memory (a by-value
+// aggregate of an out-of-line callee), and every field read from there is a scratch load whose
+// vmcnt wait would drain the helper's prefetched job stream.
+template <class Q>
+__device__ __forceinline__ Q* rfl_ptr(Q* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    return (Q*)(uintptr_t)(((uint64_t)(uint32_t)rfl((int32_t)(v >> 32)) << 32) |
+                           (uint32_t)rfl((int32_t)(uint32_t)v));
+}
+__device__ __forceinline__ MwTiles tiles_sgpr(const MwTiles& T) {
+    return MwTiles{rfl_ptr(T.tdone), (unsigned)rfl((int32_t)T.need), rfl_ptr(T.ring),
+                   rfl_ptr(T.ctl), (unsigned)rfl((int32_t)T.round), (unsigned)rfl((int32_t)T.comp),
+                   (unsigned)rfl((int32_t)T.ntj), rfl_ptr(T.feas)};
+}
+
 // ------------------------------------------------------------------------------- helper
 // Helper entry lists: MW_EPL clean candidates + UPL dirty rows per lane, each key tagged with
 // its entry index in the low bits (positions < 2^29, FIT_MAX_NODES), INF stays INF.
@@ -502,13 +579,13 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
         }
 #endif
 
-// Helper h (1..MW_H) pre-resolves jobs t = h-1, h-1+H, ...  Loads run two jobs ahead (keys, job
-// row, bound) and one job ahead (the node rows of the candidates); the three register sets are
-// indexed by literal constants only (3-way unrolled loop).
+// Helper h (1..MW_H) pre-resolves records i = h-1, h-1+H, ... (record i: the i-th live job of the
+// window, tj[] its window index).  Loads run two records ahead (keys, job row, bound) and one
+// record ahead (the node rows of the candidates); the three register sets are indexed by literal
+// constants only (3-way unrolled loop).
 #define MW_HSTEP(A, B_, C)                                                                     \
     {                                                                                          \
-        if (t >= P.w) goto hdone;                                                              \
-        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) { /* job t+H's candidates' rows */ \
+        _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) { /* record i+H's candidates' rows */\
             const uint64_t k_ = kk[B_][e];                                                     \
             const uint32_t p_ = k_ != KEY_INF ? (uint32_t)k_ : (uint32_t)P.nb;                 \
             const NodeRec r_ = ld_node(rec + p_);                                              \
@@ -520,8 +597,11 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
             ro[B_][e] = r_.orig;                                                               \
         }                                                                                      \
         {                                                                                      \
-            const int tt_ = min(t + 2 * MW_H, wlast) + z;                                      \
             MW_CLK(tw0_);                                                                      \
+            int tn_;                                                                           \
+            if (!mw_skip_live(T, P, cur, ready, S, MW_H, tn_)) goto hdone;                     \
+            tj[C] = tn_;                                                                       \
+            const int tt_ = min(tn_, wlast) + z;                                               \
             if (!mw_tile_ready(T, tt_, ready, S)) goto hdone;                                  \
             {                                                                                  \
                 MW_CLK(tw1_);                                                                  \
@@ -532,13 +612,13 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
             jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
             jbd[C] = bnd[P.slot0 + tt_];                                                       \
         }                                                                                      \
-        /* snapshot: the decider has resolved at least t - (MW_M - 1) jobs (and so has read  \
-           record slot t & 7's previous job) */                                                \
+        /* snapshot: the decider has resolved at least i - (MW_M - 1) records (and so has read  \
+           record slot i & 7's previous one) */                                                \
         uint64_t dn_;                                                                          \
         MW_CLK(hw0_);                                                                          \
         for (unsigned sp_ = 0;; ++sp_) {                                                       \
             dn_ = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
-            const int lag_ = t - (MW_SNAP - 1) - rfl((int32_t)(uint32_t)dn_);                  \
+            const int lag_ = i - (MW_SNAP - 1) - rfl((int32_t)(uint32_t)dn_);                  \
             if (lag_ <= 0) break;                                                              \
             if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
             if (sp_ > MW_SPIN_LIMIT) {                                                         \
@@ -552,6 +632,19 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
         lds_acquire(); /* the rows / bitmap the decider released with dn_ */                   \
         const uint32_t v_ = (uint32_t)rfl((int32_t)(uint32_t)dn_);                             \
         const int nu_ = rfl((int32_t)(uint32_t)(dn_ >> 32));                                   \
+        MwRec* R_ = &S->rec[i & (MW_R - 1)];                                                   \
+        if (tj[A] >= P.w) { /* no live job left: the end record (B = 0, nothing fits) */       \
+            if (lane == 0) {                                                                   \
+                *reinterpret_cast<v4i32*>(&R_->h.cpu) = v4i32{0, 0, 0, 0};                     \
+                *reinterpret_cast<uint4*>(&R_->h.pbit) = make_uint4(0u, (uint32_t)P.w, 0u, 0u);\
+                R_->h.v = (int32_t)v_;                                                         \
+                R_->h.n = 0;                                                                   \
+                R_->h.q = -1;                                                                  \
+                lds_release();                                                                 \
+                lds_st(&R_->h.ready, (uint32_t)i + 1u);                                        \
+            }                                                                                  \
+            goto hdone;                                                                        \
+        }                                                                                      \
         {                                                                                      \
             MW_CLK(hw1_);                                                                      \
             MW_ACC(a_hw, hw1_ - hw0_);                                                         \
@@ -570,19 +663,18 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
         }                                                                                      \
         uint64_t xd[UPL_MW];                                                                   \
         MwRow wr_[UPL_MW];                                                                     \
-        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) {                                   \
-            xd[i] = KEY_INF;                                                                   \
-            wr_[i] = MwRow{0, 0, 0, 0, 0u, 0u, 0, 0};                                          \
-            const int u_ = i * 64 + lane;                                                      \
-            if (i * 64 < nu_) { /* uniform: rows [0, nu) exist */                              \
-                wr_[i] = S->rows[u_ < nu_ ? u_ : 0];                                           \
-                const uint64_t y_ = mw_key(wr_[i].cpu, wr_[i].mem, wr_[i].gpu, wr_[i].avail,   \
-                                           wr_[i].mask, wr_[i].pos, J_.cpu, J_.mem, J_.gpu,    \
+        _Pragma("unroll") for (int u = 0; u < UPL_MW; ++u) {                                   \
+            xd[u] = KEY_INF;                                                                   \
+            wr_[u] = MwRow{0, 0, 0, 0, 0u, 0u, 0, 0};                                          \
+            const int u_ = u * 64 + lane;                                                      \
+            if (u * 64 < nu_) { /* uniform: rows [0, nu) exist */                              \
+                wr_[u] = S->rows[u_ < nu_ ? u_ : 0];                                           \
+                const uint64_t y_ = mw_key(wr_[u].cpu, wr_[u].mem, wr_[u].gpu, wr_[u].avail,   \
+                                           wr_[u].mask, wr_[u].pos, J_.cpu, J_.mem, J_.gpu,    \
                                            J_.wall, J_.pbit);                                  \
-                xd[i] = u_ < nu_ && y_ <= Bd_ ? y_ : KEY_INF;                                  \
+                xd[u] = u_ < nu_ && y_ <= Bd_ ? y_ : KEY_INF;                                  \
             }                                                                                  \
         }                                                                                      \
-        MwRec* R_ = &S->rec[t & (MW_R - 1)];                                                   \
         int n_ = 0;                                                                            \
         {                                                                                      \
             MW_CLK(hx_);                                                                       \
@@ -593,12 +685,12 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
            plus a predicated shift in the winning lane */                                      \
         uint64_t q_[MW_NE];                                                                    \
         _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e) q_[e] = mw_tag(x0[e], e);           \
-        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) q_[MW_EPL + i] = mw_tag(xd[i], MW_EPL + i);\
+        _Pragma("unroll") for (int u = 0; u < UPL_MW; ++u) q_[MW_EPL + u] = mw_tag(xd[u], MW_EPL + u);\
         mw_sort(q_);                                                                           \
         /* item index + 1 of each entry, 4 bits per entry (0: not taken) */                     \
         uint32_t sel_ = 0u;                                                                    \
-        /* at most t - v nodes can change before job t is decided: t - v + 1 items suffice */  \
-        const int nmax_ = min(MW_M, t - (int)v_ + 1);                                          \
+        /* at most i - v nodes can change before record i is decided: i - v + 1 items suffice */\
+        const int nmax_ = min(MW_M, i - (int)v_ + 1);                                          \
         MW_EXTRACT                                                                             \
         /* items: the lanes that gave an entry store it (exec-masked: only those lanes use   \
            the LDS, which the decider shares) */                                               \
@@ -609,22 +701,22 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
                                           ro[A][e], rc[A][e], rm[A][e], rg[A][e], ra[A][e],    \
                                           rk[A][e], 0u, 0u, 0u};                               \
         }                                                                                      \
-        _Pragma("unroll") for (int i = 0; i < UPL_MW; ++i) {                                   \
-            const uint32_t ix_ = (sel_ >> (4 * (MW_EPL + i))) & 15u;                           \
+        _Pragma("unroll") for (int u = 0; u < UPL_MW; ++u) {                                   \
+            const uint32_t ix_ = (sel_ >> (4 * (MW_EPL + u))) & 15u;                           \
             if (ix_)                                                                           \
-                R_->it[ix_ - 1u] = MwItem{(uint32_t)xd[i], (uint32_t)(xd[i] >> 32),            \
-                                          i * 64 + lane, wr_[i].orig, wr_[i].cpu, wr_[i].mem,  \
-                                          wr_[i].gpu, wr_[i].avail, wr_[i].mask, 0u, 0u, 0u};  \
+                R_->it[ix_ - 1u] = MwItem{(uint32_t)xd[u], (uint32_t)(xd[u] >> 32),            \
+                                          u * 64 + lane, wr_[u].orig, wr_[u].cpu, wr_[u].mem,  \
+                                          wr_[u].gpu, wr_[u].avail, wr_[u].mask, 0u, 0u, 0u};  \
         }                                                                                      \
         if (lane == 0) {                                                                       \
             *reinterpret_cast<v4i32*>(&R_->h.cpu) = v4i32{J_.cpu, J_.mem, J_.gpu, J_.wall};    \
             *reinterpret_cast<uint4*>(&R_->h.pbit) =                                           \
-                make_uint4(J_.pbit, 0u, (uint32_t)Bd_, (uint32_t)(Bd_ >> 32));                 \
+                make_uint4(J_.pbit, (uint32_t)tj[A], (uint32_t)Bd_, (uint32_t)(Bd_ >> 32));    \
             R_->h.v = (int32_t)v_;                                                             \
             R_->h.n = n_;                                                                      \
             R_->h.q = J_.q;                                                                    \
             lds_release(); /* items and header before the ready word */                        \
-            lds_st(&R_->h.ready, (uint32_t)t + 1u);                                            \
+            lds_st(&R_->h.ready, (uint32_t)i + 1u);                                            \
         }                                                                                      \
         {                                                                                      \
             MW_CLK(hp1_);                                                                      \
@@ -632,14 +724,15 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
         }                                                                                      \
         MW_ACC(a_hn, 1);                                                                       \
         MW_ACC(a_hi, n_);                                                                      \
-        t += MW_H;                                                                             \
+        i += MW_H;                                                                             \
     }
 
 __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
                                        const NodeRec* __restrict__ rec_,
                                        const uint64_t* __restrict__ cand_,
                                        const uint64_t* __restrict__ bnd_,
-                                       const JobRec* __restrict__ wjob_, int h, MwTiles T) {
+                                       const JobRec* __restrict__ wjob_, int h, MwTiles Tin) {
+    const MwTiles T = tiles_sgpr(Tin);
     const GAS NodeRec* const rec = gview(rec_);
     const GAS uint64_t* const cand = gview(cand_);
     const GAS uint64_t* const bnd = gview(bnd_);
@@ -659,16 +752,20 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     }
     const int wlast = P.w - 1;
     const int z = opaque_zero();
-    int t = rfl(h - 1);  // uniform (h arrives in a VGPR: the callee is out of line)
+    const int hh = rfl(h);  // uniform (h arrives in a VGPR: the callee is out of line)
+    int i = hh - 1;         // record index
 
     uint64_t kk[3][MW_EPL], jbd[3];
     JobRec jr[3];
     int32_t rc[3][MW_EPL], rm[3][MW_EPL], rg[3][MW_EPL], ra[3][MW_EPL], ro[3][MW_EPL];
     uint32_t rk[3][MW_EPL];
+    int tj[3];      // window index of the job of each register set (P.w: past the last live job)
     int ready = 0;  // scan tiles known complete
+    MwCursor cur{-1, 0ull};
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {  // jobs t and t + H
-        const int tt = min(t + s * MW_H, wlast) + z;
+    for (int s = 0; s < 2; ++s) {  // records i and i + H
+        if (!mw_skip_live(T, P, cur, ready, S, s == 0 ? hh : MW_H, tj[s])) return;
+        const int tt = min(tj[s], wlast) + z;
         if (!mw_tile_ready(T, tt, ready, S)) return;  // halted / watchdog
 #pragma unroll
         for (int e = 0; e < MW_EPL; ++e)
@@ -690,7 +787,7 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
     MW_DECL(a_hw);
     MW_DECL(a_hn);
     MW_DECL(a_hi);
-    MW_DECL(a_ht);  // waiting for scan tiles (prefetch of job t + 2H)
+    MW_DECL(a_ht);  // waiting for scan tiles (prefetch of record i + 2H)
     MW_DECL(a_hp);  // snapshot → record published
     MW_DECL(a_hx);  // snapshot → extraction start (dirty rows read, candidates filtered)
     MW_CLK(h0);
@@ -731,7 +828,8 @@ struct MwRecRegs {  // one record as this lane sees it: header (every lane) and 
 };
 
 struct MwDec {
-    int t, nu, placed, stop;
+    int t, nu, placed, stop;  // t: records decided (live jobs)
+    int done;                 // window jobs resolved when the walk ended (its stop / end record)
     bool exit;  // the window is finished (end, stop or watchdog): later steps change nothing
 #ifdef MW_SEGSTAMP
     unsigned long long seg[8], prev;
@@ -780,7 +878,9 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                                           uint64_t& waitcyc) {
     const int lane = threadIdx.x & 63;
     const int t = D.t;
-    if (t >= P.w) D.exit = true;
+#ifdef MW_DECIDER_BENCH
+    if (t >= P.w) D.exit = true;  // pre-filled records: no end record
+#endif
     MW_SEG(D, 0);
     // publish the decisions so far (the previous job's row / bitmap writes were issued before
     // record t's reads, all of which are complete here): release store of {decided, nu}
@@ -884,7 +984,10 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
             d = decide(cur);
         }
         if (!D.exit && (d.stopB || d.full)) {
-            D.stop = d.stopB ? 1 : 2;  // candidate list exhausted (rescan) / dirty set full
+            // the end record (no live job left: B = 0, nothing fits) or a stop at the record's
+            // job: candidate list exhausted (rescan) / dirty set full
+            D.done = (int32_t)cur.h2.y;
+            if (D.done < P.w) D.stop = d.stopB ? 1 : 2;
             D.exit = true;
         }
     }
@@ -983,7 +1086,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
 #ifndef MW_NO_SETPRIO
     __builtin_amdgcn_s_setprio(3);  // shares its SIMD with a helper wave
 #endif
-    MwDec D{0, 0, 0, 0, false};
+    MwDec D{0, 0, 0, 0, 0, false};
 #ifdef MW_SEGSTAMP
     for (int i = 0; i < 8; ++i) D.seg[i] = 0;
     D.prev = 0;
@@ -1045,7 +1148,10 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
 #endif
     MW_ADD(1, waitcyc);
     MW_ADD(2, t);
-    return CommitResult{t, D.stop, D.nu, D.placed};
+#ifdef MW_DECIDER_BENCH
+    D.done = t;
+#endif
+    return CommitResult{D.done, D.stop, D.nu, D.placed};
 }
 
 // All MW_WAVES waves of the block call this; returns the same result in every wave.

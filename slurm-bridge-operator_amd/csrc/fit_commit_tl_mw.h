@@ -282,7 +282,8 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
                                        const uint64_t* __restrict__ cand_,
                                        const uint64_t* __restrict__ bnd_,
                                        const JobRec* __restrict__ wjob_, int h, int32_t H,
-                                       MwTiles T) {
+                                       MwTiles Tin) {
+    const MwTiles T = tiles_sgpr(Tin);  // no scratch loads in the loop (fit_commit_mw.h)
     const GAS Seg* const slab = gview(slab_);
     const GAS TlHdr* const hdr = gview(hdr_);
     const GAS uint64_t* const cand = gview(cand_);

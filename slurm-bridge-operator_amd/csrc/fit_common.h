@@ -164,7 +164,8 @@ __device__ __forceinline__ void scan_tile(
     const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
     const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
     const uint16_t* __restrict__ jk, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
-    JobRec* __restrict__ wjob, uint64_t (*xk)[K][64]) {
+    JobRec* __restrict__ wjob, uint64_t (*xk)[K][64],
+    unsigned long long* __restrict__ feas = nullptr) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -215,6 +216,10 @@ __device__ __forceinline__ void scan_tile(
             merge_lists(key, o);
         }
         __syncthreads();
+    }
+    if (feas != nullptr && wave == 0) {  // the tile's jobs with a fitting node in this block-slice
+        const uint64_t fm = __ballot(active && key[0] != KEY_INF);
+        if (lane == 0 && fm != 0ull) atomicOr(feas, (unsigned long long)fm);
     }
     if (wave != 0 || !active) return;  // (no barrier follows inside scan_tile)
     uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KW;

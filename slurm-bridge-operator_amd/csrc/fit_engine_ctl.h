@@ -26,6 +26,11 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned pad2[30];
     unsigned done[32][32];  // per component tiles completed (own 128-B line each)
     unsigned tdone[32][ENGINE_TILES];  // per component, per window job tile: slices completed
+    // per component, per window job tile: bit j = job j of the tile has a node that fits it at
+    // the round's start state (OR over the block-slices; k_engine).  A job without one is
+    // unplaced whatever the round decides before it (node state only shrinks within a
+    // placement): the commit skips it (fit_commit_mw.h, "live jobs")
+    unsigned long long tfeas[32][ENGINE_TILES];
     unsigned long long pub[32];        // FIT_STAMPS: realtime of each component's last publish
 };
 

@@ -86,8 +86,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 if (lane == 0) plans[c] = P;
                 for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
-                for (unsigned i = lane; i < ntj; i += 64)
+                for (unsigned i = lane; i < ntj; i += 64) {
                     __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ctl->tfeas[c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 release_agent();  // plan, bound / counter reset and last round's node rows → visible
                 // just-in-time publishing (ENGINE_AHEAD > 0, k = 1 windows): the first
                 // ENGINE_AHEAD job tiles now, the rest by the helpers as they reach them
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax,
                                      MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
                                              jit ? ring : nullptr, ctl,
-                                             (unsigned)rounds + 1u, (unsigned)c, ntj});
+                                             (unsigned)rounds + 1u, (unsigned)c, ntj,
+                                             &ctl->tfeas[c][0]});
                 // every tile published this round (the committer's and the helpers') must be
                 // complete before the next round reuses the buffers: count them
                 if (jit && wave == 0) target += M->pubt * (unsigned)S.nslice;
@@ -234,10 +237,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0)                                             \
             scan_tile<true, (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_), K_>(                       \
                 P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,         \
-                reinterpret_cast<uint64_t(*)[(FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_)][64]>(smem)); \
+                reinterpret_cast<uint64_t(*)[(FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_)][64]>(smem), \
+                &ctl->tfeas[c][tile]);                                                            \
         else                                                                                      \
             scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand,    \
-                                bnd, wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem));          \
+                                bnd, wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem),           \
+                                &ctl->tfeas[c][tile]);                                            \
         break;
                 SCAN_K(16)
                 SCAN_K(8)
