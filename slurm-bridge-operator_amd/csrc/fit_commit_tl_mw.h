@@ -100,7 +100,9 @@ __device__ __forceinline__ T* tm_lds(T* p) {
 }
 
 #ifndef TL_AHEAD
-#define TL_AHEAD 4  // job tiles published ahead of the helper that needs them (0: all up front)
+#define TL_AHEAD 2  // job tiles published ahead of the helper that needs them (0: all up front).
+                    // C5 k_engine_tl: 1 / 2 / 4 / 8 -> 174.7 / 129.9 / 133.8 / 140.5 ms (r03d/e):
+                    // tiles past a round's stop are scanned for nothing, too few starve the helpers
 #endif
 
 // Publish the window's job tiles [pubt, upto) (uniform; lane 0 claims the range by an LDS CAS) —

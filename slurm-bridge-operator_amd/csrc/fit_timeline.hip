@@ -916,7 +916,8 @@ __global__ __launch_bounds__(64) void k_commit_tl(
 }
 
 #ifndef TL_PRIO
-#define TL_PRIO 0  // 1: each round's first job tile through the priority ring (fit_engine_ctl.h)
+#define TL_PRIO 0  // each round's first job tile through the priority ring (fit_engine_ctl.h):
+                   // 1 taken by idle workers only, 2 before any task-ring tile
 #endif
 #ifndef FIT_TL_MW
 #define FIT_TL_MW 1  // 0: the single-wave committer (commit_tl_window) in k_engine_tl too
@@ -993,6 +994,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 // TL_PRIO: the first tile through the priority ring (the commit waits for it; the
                 // task ring holds other components' tiles published ahead of their need)
                 const unsigned np0 = (TL_PRIO && npub > 0) ? 1u : 0u;
+#ifdef FIT_STAMPS
+                if (lane == 0) {  // before the tasks turn visible: a worker may pick tile 0 at once
+                    __hip_atomic_store(&ctl->pub[c], __builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                }
+#endif
                 if (np0) engine_publish_prio(ctl, ring, 0u, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
                 engine_publish(ctl, ring, np0, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
                 if (FIT_TL_MW) {
@@ -1068,13 +1076,39 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     bool held = false;
     for (;;) {
         if (threadIdx.x == 0) {
-            if (!held) {
+            unsigned long long task = TASK_EXIT;
+            bool got = false;
+            // TL_PRIO 2: a round's first job tile (the commit waits for it) goes before every
+            // task-ring tile — the task ring holds the other components' tiles published ahead
+            // of their need, so behind them a first tile waited ~120 us (tools/tl_stamps.py)
+            while (TL_PRIO == 2 && !held) {
+                unsigned ph = ld_agent(&ctl->p_head);
+                if (ph >= ld_agent(&ctl->p_tail)) break;
+                if (__hip_atomic_compare_exchange_strong(&ctl->p_head, &ph, ph + 1u, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    const unsigned long long pw = (unsigned long long)(ph / PCAP + 1);
+                    for (unsigned ps = 0;; ++ps) {  // reserved before stored: a short wait
+                        const unsigned long long pg = __hip_atomic_load(
+                            ring + QCAP + (ph & (PCAP - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((pg >> 32) == pw) {
+                            task = pg;
+                            break;
+                        }
+                        if (ps > SPIN_LIMIT) {
+                            atomicOr(&ctl->error, 1u);
+                            break;
+                        }
+                    }
+                    got = true;
+                    break;
+                }
+            }
+            if (!got && !held) {
                 idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 held = true;
             }
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
-            unsigned long long task = TASK_EXIT;
-            for (unsigned spins = 0;; ++spins) {
+            for (unsigned spins = 0; !got; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1085,7 +1119,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 }
                 // TL_PRIO: while its own tile is not yet published, an idle worker takes a
                 // round's first tile from the priority ring (the claimed index stays held)
-                if (TL_PRIO) {
+                if (TL_PRIO != 0) {
                     unsigned ph = ld_agent(&ctl->p_head);
                     if (ph < ld_agent(&ctl->p_tail)) {
                         if (__hip_atomic_compare_exchange_strong(&ctl->p_head, &ph, ph + 1u, __ATOMIC_RELAXED,
@@ -1140,6 +1174,14 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
                          slot_min, xk);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+#ifdef FIT_STAMPS
+            if (threadIdx.x == 0 && tile == 0) {  // a round's first tile: pickup delay, scan time
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                atomicAdd(&g_tlsc[5], (unsigned long long)t0 - ctl->pub[c]);
+                atomicAdd(&g_tlsc[6], now - (unsigned long long)t0);
+                atomicAdd(&g_tlsc[7], 1ull);
+            }
+#endif
             const int a = P.sb + s * SCAN_WAVES * P.sub, b = min(P.se, a + SCAN_WAVES * P.sub);
             scanned += (int64_t)max(min(SCAN_JOBS, P.w - tile * SCAN_JOBS), 0) * max(b - a, 0);
         }

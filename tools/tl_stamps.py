@@ -50,5 +50,8 @@ else:  # single-wave commit
     print(f"dirty-eval split: fast {tot[8] / j:.0f}, walk {tot[9] / j:.0f} (walks per job {tot[10] / j:.2f}), "
           f"reduce {(tot[1] - tot[8] - tot[9]) / j:.0f}")
 sc = buf[64 * 12:64 * 12 + 8]
+if sc[7]:
+    print(f"round's first tile: pickup delay {sc[5] / sc[7] / 100:.1f} us, scan {sc[6] / sc[7] / 100:.1f} us "
+          f"(per task, {sc[7]} tasks)")
 print(f"scan: waves {sc[4]}, nodes/wave {sc[1] / max(sc[4], 1):.0f}, cycles/node {sc[0] / max(sc[1], 1):.0f}, "
       f"long-walk batches/node {sc[2] / max(sc[1], 1):.2f}, nodes with > 4 runs {sc[3] / max(sc[1], 1):.2%}")
