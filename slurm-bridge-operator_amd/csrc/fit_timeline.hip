@@ -62,7 +62,17 @@ struct TlWalk {
     int32_t ra, mc, mm, mg, a;  // start of the current feasible stretch (-1: none), its minima, run start
     uint64_t key;
     bool live;
+    // TL_KEY_LATE: the first d-slot stretch's start and minima, frozen when it completes; the
+    // key is packed once after the walk (tl_walk_key) instead of at every run
+    int32_t kra, kmc, kmm, kmg;
+    bool got;
 };
+#ifndef TL_KEY_LATE
+#define TL_KEY_LATE 1  // 0: the key packed at every step and selected (round-2 form)
+#endif
+__device__ __forceinline__ TlWalk tl_walk0(bool live) {
+    return TlWalk{-1, 0, 0, 0, 0, KEY_INF, live, 0, 0, 0, 0, false};
+}
 
 // One run: extend / break the feasible stretch; a stretch of d slots gives the key.  A lane
 // stops once every start it could still find is later than `lim` (the start of its cut key).
@@ -80,9 +90,18 @@ __device__ __forceinline__ void tl_step_v(TlWalk& w, bool vld, int32_t end, int3
     const int32_t mc = nw ? c : min(w.mc, c), mm = nw ? m : min(w.mm, m), mg = nw ? g : min(w.mg, g);
     const bool done = f & (end - ra >= d);
     const bool kill = f ? (ra > lim) : ((end + d > H) | (end > lim));
-    const uint64_t k = tl_key(ra, mc, mm, mg, jc, jm, jg, pos);
     const bool lv = w.live & vld;
+#if TL_KEY_LATE
+    const bool fin = lv & done;
+    w.kra = fin ? ra : w.kra;
+    w.kmc = fin ? mc : w.kmc;
+    w.kmm = fin ? mm : w.kmm;
+    w.kmg = fin ? mg : w.kmg;
+    w.got = w.got | fin;
+#else
+    const uint64_t k = tl_key(ra, mc, mm, mg, jc, jm, jg, pos);
     w.key = (lv & done) ? k : w.key;
+#endif
     w.live = vld ? (w.live & !done & !kill) : w.live;
     w.ra = ra;
     w.mc = mc;
@@ -115,6 +134,11 @@ __device__ __forceinline__ void tl_step(TlWalk& w, int32_t end, int32_t c, int32
         }
         if (end - w.ra >= d) {
             w.key = tl_key(w.ra, w.mc, w.mm, w.mg, jc, jm, jg, pos);
+            w.kra = w.ra;
+            w.kmc = w.mc;
+            w.kmm = w.mm;
+            w.kmg = w.mg;
+            w.got = true;
             w.live = false;
         } else if (w.ra > lim) {
             w.live = false;
@@ -126,13 +150,23 @@ __device__ __forceinline__ void tl_step(TlWalk& w, int32_t end, int32_t c, int32
     w.a = end;
 }
 
+// the walk's key (KEY_INF: no window found)
+__device__ __forceinline__ uint64_t tl_walk_key(const TlWalk& w, int32_t jc, int32_t jm,
+                                                int32_t jg, uint32_t pos) {
+#if TL_KEY_LATE
+    return w.got ? tl_key(w.kra, w.kmc, w.kmm, w.kmg, jc, jm, jg, pos) : KEY_INF;
+#else
+    return w.key;
+#endif
+}
+
 // Earliest start of a d-slot window whose every run holds (jc, jm, jg), and its key, for `live`
 // lanes walking their node's runs [0, cnt) (any address space; the loop is wave-uniform).
 __device__ __forceinline__ uint64_t tl_eval(const Seg* sg, int cnt, bool live, int32_t jc,
                                             int32_t jm, int32_t jg, int32_t d, int32_t H,
                                             uint32_t pos, uint64_t cut) {
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
-    TlWalk w{-1, 0, 0, 0, 0, KEY_INF, live && d <= H};
+    TlWalk w = tl_walk0(live && d <= H);
     for (int i = 0;; ++i) {
         if (!__ballot(w.live && i < cnt)) break;
         if (w.live && i < cnt) {
@@ -140,7 +174,7 @@ __device__ __forceinline__ uint64_t tl_eval(const Seg* sg, int cnt, bool live, i
             tl_step(w, g.end, g.cpu, g.mem, g.gpu, jc, jm, jg, d, H, lim, pos);
         }
     }
-    return w.key;
+    return tl_walk_key(w, jc, jm, jg, pos);
 }
 
 // Same walk, four runs per step (one round trip for four reads, one ballot per four runs).
@@ -149,7 +183,7 @@ __device__ __forceinline__ uint64_t tl_eval4(const Seg* sg, int cnt, int cap, bo
                                              int32_t jm, int32_t jg, int32_t d, int32_t H,
                                              uint32_t pos, uint64_t cut) {
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
-    TlWalk w{-1, 0, 0, 0, 0, KEY_INF, live && d <= H};
+    TlWalk w = tl_walk0(live && d <= H);
     for (int i = 0;; i += 4) {
         if (!__ballot(w.live && i < cnt)) break;
         Seg g[4];
@@ -164,7 +198,7 @@ __device__ __forceinline__ uint64_t tl_eval4(const Seg* sg, int cnt, int cap, bo
 #endif
         }
     }
-    return w.key;
+    return tl_walk_key(w, jc, jm, jg, pos);
 }
 
 // ------------------------------------------------------------------------------ k_build_tl
@@ -243,9 +277,8 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
                                              unsigned long long& batches) {
     const uint64_t cut = key[TL_KS - 1];
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
-    TlWalk w{-1, 0, 0, 0, 0, KEY_INF,
-             (h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu && J.mem <= h.mem &&
-                 J.gpu <= h.gpu};
+    TlWalk w = tl_walk0((h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu &&
+                        J.mem <= h.mem && J.gpu <= h.gpu);
     const int cn = __builtin_amdgcn_readfirstlane(h.cnt);
 #pragma unroll
     for (int i = 0; i < TL_HEAD; ++i)
@@ -267,7 +300,8 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
                             J.wall, H, lim, (uint32_t)x);
         }
     }
-    if (w.key < key[TL_KS - 1]) topk_insert(key, w.key);
+    const uint64_t wk = tl_walk_key(w, J.cpu, J.mem, J.gpu, (uint32_t)x);
+    if (wk < key[TL_KS - 1]) topk_insert(key, wk);
 }
 
 // One scan tile: SCAN_JOBS window jobs × block-slice s of the component (host-driven k_scan_tl

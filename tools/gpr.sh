@@ -1,9 +1,10 @@
 #!/bin/bash
-# gpurun with retries only when no box was obtained (exit 3: nothing ran, nothing charged)
+# gpurun, retried only when the call never ran on a box (no box / slot free, or the box was lost
+# before the command started: gpurun reports status=transient and charges nothing)
 LOG=$1; shift
-for k in 1 2 3 4 5 6; do
+for k in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun "$@" > $LOG 2>&1; rc=$?
-  [ $rc -ne 3 ] && exit $rc
-  sleep 90
+  grep -q "status=transient" $LOG || exit $rc
+  sleep 60
 done
 exit 3
