@@ -75,14 +75,16 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg*
                             CommitResult* res, int32_t H, int32_t R);
 int engine_tl_runs(int32_t max_component_nodes);
 size_t engine_tl_lds_bytes(int32_t max_component_nodes);
-int engine_tl_blocks_per_cu(size_t lds);
+int engine_tl_blocks_per_cu(size_t lds, int mode);
+size_t engine_tl_scan_lds_bytes();
 hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
                             const void* cs, void* co, CompPlan* plans, int ncomp, Seg* slab,
                             TlHdr* hdr, const int32_t* jl, const int32_t* jcpu,
                             const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
                             const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
                             const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
-                            int32_t slot_min, int32_t R, int64_t* wbusy);
+                            int32_t slot_min, int32_t R, int64_t* wbusy, int mode,
+                            unsigned* resident);
 hipError_t launch_expand_tl(hipStream_t st, const int32_t* perm, const Seg* slab,
                             const TlHdr* hdr, int32_t nn, int32_t H, int32_t* oc, int32_t* om,
                             int32_t* og);
@@ -204,6 +206,10 @@ struct fit_ctx {
     HBuf<uint64_t> h_count;
     hipStream_t st = nullptr;
     hipEvent_t ev[6] = {};
+    // FIT_TL_SPLIT: the backfill engine's scan workers as a second, concurrent launch
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_join = nullptr;
+    unsigned* resident = nullptr;  // host-mapped: committer blocks running
     int wmin = 256, wmax = 8192;
 
     // node table
@@ -286,6 +292,9 @@ struct fit_ctx {
         h_err.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (resident) (void)hipHostFree(resident);
+        if (st2) (void)hipStreamDestroy(st2);
         if (st) (void)hipStreamDestroy(st);
         if (comm) (void)ncclCommDestroy(comm);
     }
@@ -765,19 +774,60 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
                         nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     }
     const size_t lds = engine_tl_lds_bytes(maxnodes);
-    const int per_cu = engine_tl_blocks_per_cu(lds);
+    // FIT_TL_SPLIT: committers and scan workers as two concurrent launches (fit_timeline.hip
+    // k_engine_tl_t): the workers' launch carries only the scan's registers and LDS, so several
+    // worker blocks share a CU instead of one block per CU for everything
+    bool split = FIT_TL_SPLIT_DEF != 0;
+    if (const char* e = getenv("FIT_TL_SPLIT")) split = atoi(e) != 0;
+    const size_t lds_w = split ? engine_tl_scan_lds_bytes() : lds;
+    const int per_cu = engine_tl_blocks_per_cu(lds, split ? 1 : 0);
     if (per_cu <= 0) return fail(FIT_E_HIP, "k_engine_tl does not fit on a CU (lds %zu)", lds);
-    int workers = std::max(8, per_cu * c->cus - nc);
+    const int per_cu_w = split ? engine_tl_blocks_per_cu(lds_w, 2) : per_cu;
+    if (per_cu_w <= 0) return fail(FIT_E_HIP, "k_engine_tl workers do not fit on a CU");
+    int workers = split ? std::max(8, per_cu_w * std::max(1, c->cus - nc)) : std::max(8, per_cu * c->cus - nc);
     if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
+    if (split && !c->st2) {
+        if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(&c->resident, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return fail(FIT_E_HIP, "split launch: stream / event / mapped flag");
+    }
     if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers)) return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
     HIP_TRY(hipEventRecord(c->ev[0], st));
-    HIP_TRY(launch_engine_tl(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
-                             c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
-                             part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
-                             c->tl_slots, c->tl_slot_min, R, c->ebusy.p));
+    bool resident_late = false;
+    if (!split) {
+        HIP_TRY(launch_engine_tl(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
+                                 c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
+                                 part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
+                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 0, nullptr));
+    } else {
+        __atomic_store_n(c->resident, 0u, __ATOMIC_RELEASE);
+        unsigned* dres = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dres), c->resident, 0));
+        HIP_TRY(launch_engine_tl(nc, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p, c->plan.p,
+                                 nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall, part,
+                                 c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs, c->tl_slots,
+                                 c->tl_slot_min, R, c->ebusy.p, 1, dres));
+        // the workers go in once every committer block holds its CU (a worker block on a CU
+        // would leave a committer no room, and the committers' rounds wait for workers)
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(c->resident, __ATOMIC_ACQUIRE) < (unsigned)nc) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                resident_late = true;  // launched anyway: the kernels' own watchdogs end it
+                break;
+            }
+        }
+        HIP_TRY(hipStreamWaitEvent(c->st2, c->ev[0], 0));  // after the control-block resets
+        HIP_TRY(launch_engine_tl(workers, lds_w, c->st2, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
+                                 c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
+                                 part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
+                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 2, nullptr));
+        HIP_TRY(hipEventRecord(c->ev_join, c->st2));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
@@ -785,6 +835,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->h_err.p[0]) return fail(FIT_E_HIP, "timeline engine watchdog tripped (code %u)", c->h_err.p[0]);
+    if (resident_late) return fail(FIT_E_HIP, "timeline engine: committer blocks not resident after 10 s");
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device += ms;

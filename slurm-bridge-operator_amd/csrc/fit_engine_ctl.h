@@ -6,7 +6,10 @@
 
 namespace fitgpu {
 
-constexpr unsigned QCAP = 1u << 16;  // task ring entries (8-byte {epoch, tile} granules)
+#ifndef FIT_QCAP_LOG2
+#define FIT_QCAP_LOG2 16
+#endif
+constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
 constexpr unsigned PCAP = 1u << 12;  // priority ring entries (after the task ring): each round's first tile
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
 constexpr unsigned SPIN_LIMIT = 1u << 25;

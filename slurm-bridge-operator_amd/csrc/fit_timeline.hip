@@ -966,7 +966,14 @@ namespace fitgpu {
 // component's rounds (publish its scan tiles to the device task ring, wait for them, commit the
 // window with commit_tl_window); blocks [C, C+W) are scan workers running scan_tile_tl.
 // Components advance at their own pace and their scans share the chip; no host round trips.
-__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
+// MODE 0: one launch holds both (blocks [0, C) commit, the rest scan); MODE 1 / 2: the committers
+// and the scan workers as two concurrent launches (FIT_TL_SPLIT, engine.cpp): the workers' launch
+// then carries only the scan's registers and LDS, so several worker blocks share a CU (one block
+// per CU when the committer's 160 KB of LDS and its helpers' VGPRs size every block of the launch).
+// A MODE 1 block counts itself into `resident` (host-mapped) so that the host launches the
+// workers only once every committer holds its CU.
+template <int MODE>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl_t(
     EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
     const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
     int ncomp, Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
@@ -975,11 +982,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
     JobRec* __restrict__ wjob, const int32_t* __restrict__ perm, int32_t* __restrict__ out,
     int32_t* __restrict__ outs, int32_t H, int32_t slot_min, int32_t R,
-    int64_t* __restrict__ wbusy) {
+    int64_t* __restrict__ wbusy, unsigned* __restrict__ resident) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
 
-    if ((int)blockIdx.x < ncomp) {
+    if (MODE == 1 || (MODE == 0 && (int)blockIdx.x < ncomp)) {
+        if (MODE == 1 && threadIdx.x == 0)
+            __hip_atomic_fetch_add(resident, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // ================================================================ committer
         // FIT_TL_MW: wave 0 runs the round protocol (publish the window's tiles), then all 8
         // waves commit it (fit_commit_tl_mw.h: wave 0 decides, waves 1..7 pre-resolve);
@@ -1190,8 +1199,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const unsigned long long task = *task_slot;
         if (task == TASK_EXIT) {  // block-uniform
             if (threadIdx.x == 0) {
-                wbusy[2 * (blockIdx.x - ncomp)] = busy;
-                wbusy[2 * (blockIdx.x - ncomp) + 1] = scanned;
+                const int wi = MODE == 2 ? (int)blockIdx.x : (int)blockIdx.x - ncomp;
+                wbusy[2 * wi] = busy;
+                wbusy[2 * wi + 1] = scanned;
             }
             return;
         }
@@ -1353,13 +1363,15 @@ size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
     return std::max(commit, scan);
 }
 
-int engine_tl_blocks_per_cu(size_t lds) {
+int engine_tl_blocks_per_cu(size_t lds, int mode) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl, SCAN_WAVES * 64, lds) !=
-        hipSuccess)
-        return 0;
-    return n;
+    const hipError_t e =
+        mode == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<2>, SCAN_WAVES * 64, lds)
+        : mode == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<1>, SCAN_WAVES * 64, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<0>, SCAN_WAVES * 64, lds);
+    return e == hipSuccess ? n : 0;
 }
+size_t engine_tl_scan_lds_bytes() { return sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16; }
 
 hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
                             const void* cs, void* co, CompPlan* plans, int ncomp, Seg* slab,
@@ -1367,12 +1379,18 @@ hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, v
                             const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
                             const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
                             const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
-                            int32_t slot_min, int32_t R, int64_t* wbusy) {
-    hipLaunchKernelGGL(k_engine_tl, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,
-                       static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),
-                       static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,
-                       slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, perm, out,
-                       outs, H, slot_min, R, wbusy);
+                            int32_t slot_min, int32_t R, int64_t* wbusy, int mode,
+                            unsigned* resident) {
+#define FIT_ENGINE_TL(M_)                                                                         \
+    hipLaunchKernelGGL(k_engine_tl_t<M_>, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,          \
+                       static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),     \
+                       static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,\
+                       slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, perm, out,  \
+                       outs, H, slot_min, R, wbusy, resident)
+    if (mode == 1) FIT_ENGINE_TL(1);
+    else if (mode == 2) FIT_ENGINE_TL(2);
+    else FIT_ENGINE_TL(0);
+#undef FIT_ENGINE_TL
     return hipGetLastError();
 }
 
