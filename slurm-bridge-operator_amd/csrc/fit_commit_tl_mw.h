@@ -179,6 +179,11 @@ __device__ __forceinline__ uint64_t tm_fit0(const Seg* L, const int4* PM, int cn
 #ifndef TM_FAST
 #define TM_FAST 1  // 0: the decider's first form (4-ary ring searches, tl_reserve_lds + tl_pm_build)
 #endif
+#ifndef TM_FIT8
+#define TM_FIT8 1  // ring lists' first run ending at or after d: eight lanes per list over its first
+                   // eight runs (one LDS read, one ballot); 0: 64 lanes per list, one read and one
+                   // ballot per list
+#endif
 
 typedef __attribute__((address_space(3))) v4i32 lds_v4i32;
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
@@ -543,6 +548,7 @@ struct TmDec {
     int t, nu, placed, stop;
     uint64_t gm;  // dirty slots whose list lives in the global slab
     uint32_t rb[TM_R];  // LDS byte address of ring entry i's run-list region (uniform)
+    uint32_t rbv;       // the same per lane: lane l holds rb[l >> 3] (TM_FIT8)
     bool exit;
 #ifdef FIT_STAMPS
     unsigned long long acc[10];
@@ -594,15 +600,27 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         // lane i reads list i's prefix minima there
         uint64_t rk;
         {
-            const uint32_t lo = 16u * (uint32_t)min(lane, X.R - 1);
-            int32_t ev[TM_R];
-#pragma unroll
-            for (int i = 0; i < TM_R; ++i) ev[i] = lds_ld1(D.rb[i] + lo);
             int32_t kk = 0;
+#if TM_FIT8
+            // lane l: run l & 7 of ring list l >> 3; lane i < 8 takes the first set bit of byte i
+            // (a list shorter than eight runs ends at H >= d, so its byte has a real run set);
+            // a live list whose first eight runs all end before d takes the general search below
+            const int32_t e8 = lds_ld1(D.rbv + 16u * (uint32_t)min(lane & 7, X.R - 1));
+            const uint64_t m8 = __ballot(e8 >= jd);
+            const uint32_t byte = (uint32_t)(m8 >> (8 * (lane & 7))) & 0xffu;
+            kk = (int32_t)__builtin_ctz(byte | 0x100u);
+            if (__builtin_expect(__ballot(lane < 8 && ok && !isg && byte == 0u) != 0ull, 0))
+#endif
+            {
+                const uint32_t lo = 16u * (uint32_t)min(lane, X.R - 1);
+                int32_t ev[TM_R];
 #pragma unroll
-            for (int i = 0; i < TM_R; ++i) {
-                const uint64_t m = __ballot(ev[i] >= jd);
-                kk = writelane(m ? (int)__builtin_ctzll(m) : 0, i, kk);
+                for (int i = 0; i < TM_R; ++i) ev[i] = lds_ld1(D.rb[i] + lo);
+#pragma unroll
+                for (int i = 0; i < TM_R; ++i) {
+                    const uint64_t m = __ballot(ev[i] >= jd);
+                    kk = writelane(m ? (int)__builtin_ctzll(m) : 0, i, kk);
+                }
             }
             const int4 pk = X.pmr[R.ro + min(kk, X.R - 1)];
             fit0 = ok && !isg && pk.x >= jc && pk.y >= jm && pk.z >= jg;
@@ -879,6 +897,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         R.job = (R.slot == slot) ? -1 : R.job;
         R.slot = writelane_c<E>(slot, R.slot);
         D.rb[E] = (uint32_t)rfl((int32_t)lds_addr(L));
+        D.rbv = ((lane >> 3) == E) ? D.rb[E] : D.rbv;
         R.ro = writelane_c<E>(slot * X.RS, R.ro);
         R.pos = (uint32_t)writelane_c<E>((int32_t)pos, (int32_t)R.pos);
         R.mask = (uint32_t)writelane_c<E>((int32_t)mask, (int32_t)R.mask);
@@ -943,6 +962,7 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     TmDec D{};
     D.exit = false;
     for (int i = 0; i < TM_R; ++i) D.rb[i] = lds_addr(X.lr);
+    D.rbv = lds_addr(X.lr);
     TmRing R{-1, 0, 0xffffffffu, 0u, 0, -1, -1};
     int32_t oq = -1, on = -1, os = -1;
     TmRecRegs ra, rb;

@@ -337,7 +337,7 @@ __device__ __forceinline__ void scan_tile_tl(
     const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
     const int n1 = min(P.se, n0 + P.sub);
     unsigned long long batches = 0, longn = 0;
-#ifdef FIT_STAMPS
+#if defined(FIT_STAMPS) && !defined(FIT_STAMPS_NOSCAN)
     const unsigned long long sc_t0 = __builtin_amdgcn_s_memtime();
 #endif
     if (n0 < n1) {
@@ -354,7 +354,7 @@ __device__ __forceinline__ void scan_tile_tl(
             }
         }
     }
-#ifdef FIT_STAMPS
+#if defined(FIT_STAMPS) && !defined(FIT_STAMPS_NOSCAN)  // NOSCAN: 5 same-address atomics per wave per task serialise in L2
     if (lane == 0) {
         atomicAdd(&g_tlsc[0], __builtin_amdgcn_s_memtime() - sc_t0);
         atomicAdd(&g_tlsc[1], (unsigned long long)max(n1 - n0, 0));
