@@ -65,6 +65,16 @@ def test_c5_full_nodes_prefix(engine, monkeypatch):
     check_tl(nodes, tline, jobs, parts)
 
 
+@pytest.mark.parametrize("nn,jj", [(256, 4096), (4096, 16384), (None, 2000)])
+def test_c5_split_launch(nn, jj, monkeypatch):
+    """FIT_TL_SPLIT: committers and scan workers as two concurrent launches (host waits for the
+    committers' residency flag before launching the workers) — same placements as the oracle."""
+    monkeypatch.setenv("FIT_ENGINE", "persistent")
+    monkeypatch.setenv("FIT_TL_SPLIT", "1")
+    nodes, tline, jobs, parts = synth.make_c5(nn, jj)
+    check_tl(nodes, tline, jobs, parts)
+
+
 def test_gpu_contention_future_starts():
     """GPU-heavy jobs on few GPU nodes: most starts are in the future (the backfill path)."""
     nodes, tline, jobs, parts = synth.make_c5(128, 4096)
