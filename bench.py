@@ -392,7 +392,7 @@ def live_traffic(workload, kernel, timeout=240):
             per = {}
             for path in __import__("glob").glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for row in csv.DictReader(open(path)):
-                    if row["Kernel_Name"].split("(")[0].split("::")[-1] == kernel:
+                    if row["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0] == kernel:
                         key = row["Dispatch_Id"]
                         per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
             if not per:

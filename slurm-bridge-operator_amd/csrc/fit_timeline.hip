@@ -973,7 +973,7 @@ namespace fitgpu {
 // A MODE 1 block counts itself into `resident` (host-mapped) so that the host launches the
 // workers only once every committer holds its CU.
 template <int MODE>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl_t(
+__global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
     const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
     int ncomp, Seg* __restrict__ slab, TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
@@ -1366,9 +1366,9 @@ size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
 int engine_tl_blocks_per_cu(size_t lds, int mode) {
     int n = 0;
     const hipError_t e =
-        mode == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<2>, SCAN_WAVES * 64, lds)
-        : mode == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<1>, SCAN_WAVES * 64, lds)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl_t<0>, SCAN_WAVES * 64, lds);
+        mode == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl<2>, SCAN_WAVES * 64, lds)
+        : mode == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl<1>, SCAN_WAVES * 64, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl<0>, SCAN_WAVES * 64, lds);
     return e == hipSuccess ? n : 0;
 }
 size_t engine_tl_scan_lds_bytes() { return sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16; }
@@ -1382,7 +1382,7 @@ hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, v
                             int32_t slot_min, int32_t R, int64_t* wbusy, int mode,
                             unsigned* resident) {
 #define FIT_ENGINE_TL(M_)                                                                         \
-    hipLaunchKernelGGL(k_engine_tl_t<M_>, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,          \
+    hipLaunchKernelGGL(k_engine_tl<M_>, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,          \
                        static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),     \
                        static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,\
                        slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, perm, out,  \

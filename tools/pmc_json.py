@@ -16,7 +16,7 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].split("::")[-1]
+    return name.split("(")[0].split("::")[-1].split("<")[0]  # k_engine_tl<0> -> k_engine_tl
 
 
 def main(prefix):
