@@ -45,6 +45,12 @@ namespace fitgpu {
 #ifndef MW_DTRIM
 #define MW_DTRIM 1  // 1: compile-time record slot, lane-E-only bookkeeping stores (see mw_decide)
 #endif
+#ifndef MW_STALE_SALU
+#define MW_STALE_SALU 0  // 1: item staleness as one 64-lane compare (item l & 7 vs ring entry l >> 3)
+                         // folded on the SALU — 13 fewer VALU, 16 more SALU per step, but the
+                         // compare's VALU -> SGPR -> SALU hand-off lands on the chain: C3 27.72 ->
+                         // 28.57 ms, C2 15.45 -> 16.00 ms (r03q); 0: eight DPP-rotated XORs
+#endif
 #ifndef MW_ITEMS
 #define MW_ITEMS 8
 #endif
@@ -818,6 +824,7 @@ struct MwRing {
     v4i32 a;       // cpu, mem, gpu, avail   (= MwRow's first 16 B)
     v4i32 b;       // mask, pos, orig, job   (= MwRow's last 16 B; job -1: dead)
     int32_t slot;  // dirty slot
+    uint32_t pg;   // MW_STALE_SALU: lane l holds entry (l >> 3)'s position (groups of 8 lanes)
 };
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
@@ -918,6 +925,26 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                                     jc, jm, jg, jw, jp);
         const uint64_t rkey = live ? rk0 : KEY_INF;
         const uint32_t ip = x.i0.x;
+#if MW_STALE_SALU
+        // item staleness: its node is in the live ring.  Lane l compares item l & 7 (the record
+        // read puts item l & 7 in lane l) with ring entry l >> 3 (R.pg); the live entries are
+        // the ones decisions [v, t) wrote — the L = t - v lanes before E, cyclically — so their
+        // groups form one rotated byte mask, and OR-folding the 64-bit compare mask down to its
+        // low byte leaves bit i = item i is stale.  (An entry killed by a later write of the same
+        // node lies inside the window too, and so does that later entry: same answer.)
+        bool stale;
+        {
+            const int L = min(t - rfl(v), 7);  // 0..7 (v >= t - 7: the helper's snapshot rule)
+            const uint64_t base = L > 0 ? (~0ull >> (64 - 8 * L)) : 0ull;
+            const int sft = 8 * ((E - L) & 7);
+            const uint64_t lg = sft ? (base << sft) | (base >> (64 - sft)) : base;
+            uint64_t m = __ballot(ip == R.pg) & lg;
+            m |= m >> 32;
+            m |= m >> 16;
+            m |= m >> 8;
+            stale = ((m >> (lane & 7)) & 1ull) != 0ull;
+        }
+#else
         // item staleness: its node is in the live ring.  Lanes 8..15 take a copy of the ring
         // (row_ror:8), so row_ror:k, k = 0..7, shows lane i < 8 every ring entry once.
         const uint32_t P0 = live ? (uint32_t)R.b.y : 0xffffffffu;  // positions are < 2^29
@@ -928,6 +955,7 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                        d4 = dpp_ror_xor<4, false>(P2, ip), d5 = dpp_ror_xor<5, false>(P2, ip),
                        d6 = dpp_ror_xor<6, false>(P2, ip), d7 = dpp_ror_xor<7, false>(P2, ip);
         const bool stale = min(min(min(d0, d1), min(d2, d3)), min(min(d4, d5), min(d6, d7))) == 0u;
+#endif
         const uint64_t ik0 = ((uint64_t)x.i0.y << 32) | ip;
         const uint64_t ikey = (lane < n && !stale) ? ik0 : KEY_INF;
         const bool tr = rkey < ikey;  // this lane's ring row beats its item
@@ -1008,6 +1036,9 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     R.a.w = writelane_c<E>(na, R.a.w);
     R.b.x = writelane_c<E>(nk, R.b.x);
     R.b.y = writelane_c<E>(pos, R.b.y);
+#if MW_STALE_SALU
+    R.pg = ((lane >> 3) == E) ? (uint32_t)rfl(pos) : R.pg;
+#endif
     R.b.z = writelane_c<E>(no, R.b.z);
     R.b.w = writelane_c<E>(placed ? t : -1, R.b.w);
     R.slot = writelane_c<E>(slot, R.slot);
@@ -1095,6 +1126,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     R.a = v4i32{0, 0, 0, 0};
     R.b = v4i32{0, -1, -1, -1};  // dead, position matching no item
     R.slot = -1;
+    R.pg = 0xffffffffu;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
     uint64_t waitcyc = 0;
     MW_CLK(d0);
