@@ -233,8 +233,8 @@ __device__ __forceinline__ int tm_reserve(uint32_t L, uint32_t PM, uint32_t tras
     const int st = head + tail - mergeL - mergeR;  // index shift of the runs after them
     const bool inr = (lane >= i0) & (lane <= i1);
     const Seg u{inr ? min(g.end, e) : g.end, inr ? rc : g.cpu, inr ? rm : g.mem, inr ? rg : g.gpu};
-    const int32_t pc = wave_scan_min(v ? u.cpu : TL_BIG), pm = wave_scan_min(v ? u.mem : TL_BIG),
-                  pg = wave_scan_min(v ? u.gpu : TL_BIG);
+    int32_t pc = v ? u.cpu : TL_BIG, pm = v ? u.mem : TL_BIG, pg = v ? u.gpu : TL_BIG;
+    wave_scan_min3(pc, pm, pg);
     const int32_t xc = wave_shr1(pc, TL_BIG), xm = wave_shr1(pm, TL_BIG), xg = wave_shr1(pg, TL_BIG);
     // every run at its new index (the two a merge drops excluded)
     const int dest = lane + (lane < i0 ? 0 : (lane > i1 ? st : sh));
@@ -848,7 +848,8 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 }
                 if (lane < cnt) L[lane] = g;
                 const Seg p = lane < cnt ? g : Seg{0, TL_BIG, TL_BIG, TL_BIG};
-                const int32_t vc = wave_scan_min(p.cpu), vm = wave_scan_min(p.mem), vg = wave_scan_min(p.gpu);
+                int32_t vc = p.cpu, vm = p.mem, vg = p.gpu;
+                wave_scan_min3(vc, vm, vg);
                 if (lane < cnt) PM[lane] = make_int4(vc, vm, vg, 0);
             }
             if (lane == 0) {

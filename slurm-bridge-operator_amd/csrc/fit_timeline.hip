@@ -429,13 +429,42 @@ __device__ __forceinline__ int32_t wave_scan_min(int32_t v) {
     return v;
 }
 
+#ifndef TL_SCAN_FUSED
+#define TL_SCAN_FUSED 1  // 0: three separate scans of a DPP move and a min per level (36 VALU)
+#endif
+// Three independent inclusive min-scans (a run list's cpu / mem / gpu columns), interleaved so
+// that each fused v_min_i32_dpp reads a VGPR written two instructions earlier (the DPP hazard's
+// two wait states, cdna_hip_programming.md) — 18 VALU and one s_nop.  A lane whose DPP source does
+// not exist (row_shr at a row's start) or whose row the row_mask leaves out keeps its value
+// (bound_ctrl not set), i.e. min(v, TL_BIG) = v, as in wave_scan_min.
+__device__ __forceinline__ void wave_scan_min3(int32_t& a, int32_t& b, int32_t& c) {
+#if TL_SCAN_FUSED
+#define TL_L3(CTL) "v_min_i32_dpp %0, %0, %0 " CTL "\n\tv_min_i32_dpp %1, %1, %1 " CTL \
+                   "\n\tv_min_i32_dpp %2, %2, %2 " CTL "\n\t"
+    asm volatile("s_nop 1\n\t"
+                 TL_L3("row_shr:1 row_mask:0xf bank_mask:0xf")
+                 TL_L3("row_shr:2 row_mask:0xf bank_mask:0xf")
+                 TL_L3("row_shr:4 row_mask:0xf bank_mask:0xf")
+                 TL_L3("row_shr:8 row_mask:0xf bank_mask:0xf")
+                 TL_L3("row_bcast:15 row_mask:0xa bank_mask:0xf")
+                 TL_L3("row_bcast:31 row_mask:0xc bank_mask:0xf")
+                 : "+v"(a), "+v"(b), "+v"(c));
+#undef TL_L3
+#else
+    a = wave_scan_min(a);
+    b = wave_scan_min(b);
+    c = wave_scan_min(c);
+#endif
+}
+
 // Prefix minima of an LDS run list (<= 64 runs): PM[i] = min over runs [0, i] per column.
 // With them, "fits from slot 0 for d slots" and that window's minimum are one search over the
 // run ends — the dirty-node fast path.
 __device__ __forceinline__ void tl_pm_build(const Seg* L, int4* PM, int n) {
     const int lane = threadIdx.x & 63;
     const Seg g = lane < n ? L[lane] : Seg{0, TL_BIG, TL_BIG, TL_BIG};
-    const int32_t vc = wave_scan_min(g.cpu), vm = wave_scan_min(g.mem), vg = wave_scan_min(g.gpu);
+    int32_t vc = g.cpu, vm = g.mem, vg = g.gpu;
+    wave_scan_min3(vc, vm, vg);
     if (lane < n) PM[lane] = make_int4(vc, vm, vg, 0);
 }
 
@@ -461,9 +490,11 @@ __device__ __forceinline__ uint64_t tl_walk_wave(const Seg* L, int n, int32_t jc
     if (st > lim) return KEY_INF;
     const int s0 = __builtin_amdgcn_readlane(sidx, w);
     const bool in = lane >= s0 && lane <= w;
-    const int32_t mc = __builtin_amdgcn_readlane(wave_scan_min(in ? g.cpu : TL_BIG), 63);
-    const int32_t mm = __builtin_amdgcn_readlane(wave_scan_min(in ? g.mem : TL_BIG), 63);
-    const int32_t mg = __builtin_amdgcn_readlane(wave_scan_min(in ? g.gpu : TL_BIG), 63);
+    int32_t sc = in ? g.cpu : TL_BIG, sm = in ? g.mem : TL_BIG, sg = in ? g.gpu : TL_BIG;
+    wave_scan_min3(sc, sm, sg);
+    const int32_t mc = __builtin_amdgcn_readlane(sc, 63);
+    const int32_t mm = __builtin_amdgcn_readlane(sm, 63);
+    const int32_t mg = __builtin_amdgcn_readlane(sg, 63);
     return tl_key(st, mc, mm, mg, jc, jm, jg, pos);
 }
 
