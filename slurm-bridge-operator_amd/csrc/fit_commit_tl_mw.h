@@ -31,6 +31,11 @@
 namespace fitgpu {
 
 constexpr int TM_M = 8;   // items per record (> snapshot lag)
+#ifndef TM_STAGE2
+#define TM_STAGE2 0  // 1: the helper also stages the record's second clean item's run list — slab
+                     // reads of new dirty lists 0.054 -> 0.007 per job, but C5 125.9 -> 129.0 ms
+                     // (r03w: the helper's record takes longer, 8 KB less LDS for run lists)
+#endif
 constexpr int TM_R = 8;   // record ring
 #ifndef TL_MW_SOLO
 #define TL_MW_SOLO 0  // 1: wave 4 (the decider's SIMD partner) idles; helpers are waves 1-3, 5-7
@@ -82,6 +87,9 @@ struct alignas(16) TmShared {
     uint32_t pad[7];
     TmRec rec[TM_R];
     Seg stage[TM_R][64];     // the run list of each record's first clean item
+#if TM_STAGE2
+    Seg stage2[TM_R][64];    // ... and of its second (the first is often written meanwhile)
+#endif
     TmSlot slot[TL_UCAP];
     Seg scr[TL_MAX_SLOTS];   // general-path scratch (tl_reserve_any)
     // followed by: run-list regions (TL_UCAP x RS Seg), their prefix minima (TL_UCAP x RS int4),
@@ -456,6 +464,24 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
                 spos = (uint32_t)readlane((int32_t)cpos[c], fl);
             }
         }
+#if TM_STAGE2
+        // the record's second clean item: the smallest item index above `first`
+        uint32_t fmin2 = 15u;
+#pragma unroll
+        for (int c = 0; c < TM_CPL; ++c) fmin2 = min(fmin2, (ixc[c] != 0u && ixc[c] != first) ? ixc[c] : 15u);
+        const uint32_t second = wave_min32_all(fmin2);
+        uint32_t spos2 = 0xffffffffu;
+        int fl2 = 0, fc2 = 0;
+#pragma unroll
+        for (int c = TM_CPL - 1; c >= 0; --c) {
+            const uint64_t fm = __ballot(ixc[c] != 0u && ixc[c] == second);
+            if (fm) {
+                fl2 = __builtin_ctzll(fm);
+                fc2 = c;
+                spos2 = (uint32_t)readlane((int32_t)cpos[c], fl2);
+            }
+        }
+#endif
         TlHdr ch[TM_CPL];
 #pragma unroll
         for (int c = 0; c < TM_CPL; ++c) {
@@ -470,6 +496,10 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         }
         const v4i32 sv = *(const GAS v4i32*)(slab + (int64_t)(spos != 0xffffffffu ? spos : nb) * TL_MAX_SLOTS + lane);
         const Seg srun{sv.x, sv.y, sv.z, sv.w};
+#if TM_STAGE2
+        const v4i32 sv2 = *(const GAS v4i32*)(slab + (int64_t)(spos2 != 0xffffffffu ? spos2 : nb) * TL_MAX_SLOTS + lane);
+        const Seg srun2{sv2.x, sv2.y, sv2.z, sv2.w};
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next job's prefetch too (older)
         TmRec* const Rr = &S->rec[t & (TM_R - 1)];
 #pragma unroll
@@ -485,10 +515,19 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
             scnt = readlane(fc == 0 ? ch[0].cnt : ch[TM_CPL - 1].cnt, fl);
             if (scnt <= R && lane < scnt) S->stage[t & (TM_R - 1)][lane] = srun;
         }
+        uint32_t spos2w = 0xffffffffu;
+        int32_t scnt2 = 0;
+#if TM_STAGE2
+        if (spos2 != 0xffffffffu) {
+            scnt2 = readlane(fc2 == 0 ? ch[0].cnt : ch[TM_CPL - 1].cnt, fl2);
+            if (scnt2 <= R && lane < scnt2) S->stage2[t & (TM_R - 1)][lane] = srun2;
+            spos2w = spos2;
+        }
+#endif
         if (lane == 0) {
             *reinterpret_cast<v4i32*>(&Rr->h.jc) = v4i32{jc, jm, jg, jd};
-            *reinterpret_cast<v4u32*>(&Rr->h.pbit) = v4u32{jp, spos, (uint32_t)scnt, 0u};
-            *reinterpret_cast<v4u32*>(&Rr->h.blo) = v4u32{(uint32_t)B, (uint32_t)(B >> 32), 0u, 0u};
+            *reinterpret_cast<v4u32*>(&Rr->h.pbit) = v4u32{jp, spos, (uint32_t)scnt, spos2w};
+            *reinterpret_cast<v4u32*>(&Rr->h.blo) = v4u32{(uint32_t)B, (uint32_t)(B >> 32), (uint32_t)scnt2, 0u};
             Rr->h.v = v;
             Rr->h.n = n;
             Rr->h.q = J.q;
@@ -695,7 +734,9 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 // ring lists on LDS that fail at slot 0: a later start can still win only if the
                 // best so far starts later than 0 — walk them (wave-wide, one list at a time)
                 if (d.anywalk && (bm == KEY_INF || (bm >> 54) > 0)) {
+#ifndef TM_COUNT_SLAB
                     TM_CNT(9, 1);
+#endif
                     const int32_t lim = bm == KEY_INF ? X.H : (int32_t)(bm >> 54);
                     const bool ok = live && !isg && (R.mask & jp) != 0u && jd <= X.H;
                     for (uint64_t m = __ballot(ok) & 0xffull; m; m &= m - 1) {
@@ -793,9 +834,17 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {  // staged by the helper
                     const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
                     g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
-                } else {  // not the record's first clean item (that one was written meanwhile)
+#if TM_STAGE2
+                } else if (cur.h2.w == pos && (int32_t)cur.h3.z == cnt) {  // the second staged list
+                    const v4u32 x = lds4(&S->stage2[t & (TM_R - 1)][lane])[0];
+                    g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
+#endif
+                } else {  // neither staged item (both written meanwhile)
                     const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
                     g = Seg{x.x, x.y, x.z, x.w};
+#ifdef TM_COUNT_SLAB  // diagnostic: new dirty lists read from the slab instead of the stage
+                    TM_CNT(9, 1);
+#endif
                 }
             }
             if (lane == 0) {
