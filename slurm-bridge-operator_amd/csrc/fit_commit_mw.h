@@ -17,6 +17,12 @@
 // row or bitmap word the helper read after the snapshot: any node changed after v is in the live
 // ring, so a torn or newer read of it only produces an item the decider drops.
 //
+// "Jobs" above are the window's LIVE jobs (round 3): a job that no node fits at the round's start
+// is unplaced whatever the decisions before it, so the helpers skip it (per-tile feasibility
+// masks from the scan, mw_skip_live) and record i, ring lane i & 7 and the snapshot counts all
+// index the i-th live job; the record header carries its window index, and a record whose index
+// is the window size ends the window.
+//
 // Cost model (measured on gfx950, tools/ubench: one wave alone) — what shapes the code below:
 // a dependent VALU op ≈ 4.7 cycles, any scalar branch ≈ 25-30, a VALU → SGPR → SALU hand-off
 // ≈ 20-36, v_readlane → v_writelane ≈ 8.6, one LDS round trip ≈ 50-64.  So the decider's job
