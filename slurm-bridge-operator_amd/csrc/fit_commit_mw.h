@@ -51,6 +51,11 @@ namespace fitgpu {
 #ifndef MW_DTRIM
 #define MW_DTRIM 1  // 1: compile-time record slot, lane-E-only bookkeeping stores (see mw_decide)
 #endif
+#ifndef MW_EARLYREC
+#define MW_EARLYREC 0  // 1: read record t+1's data with its ready word at the start of step t —
+                       // C3 27.68 vs 27.66 / 27.63 ms, C2 15.46 vs 15.43 (r03z): the mid-step read
+                       // was not exposed; the acquire form is kept
+#endif
 #ifndef MW_STALE_SALU
 #define MW_STALE_SALU 0  // 1: item staleness as one 64-lane compare (item l & 7 vs ring entry l >> 3)
                          // folded on the SALU — 13 fewer VALU, 16 more SALU per step, but the
@@ -909,6 +914,16 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     const MwRec* Rn = &S->rec[(t + 1) & (MW_R - 1)];
 #endif
     const uint32_t flag_n = lds_ld(&Rn->h.ready);
+#if MW_EARLYREC
+    // record t+1's data right behind its ready word, a whole step before it is used: one wave's
+    // LDS requests are served in order and the helper stores the ready word only after its data
+    // stores have completed (release = lgkmcnt(0) before it), so if this ready word reads t + 2 the
+    // data reads that follow it see the record; if not, job t+1 takes the slow path, which waits
+    // for the word, acquires and reads the record again.  The empty asm keeps the compiler from
+    // hoisting the data reads above the ready word.
+    asm volatile("" ::: "memory");
+    mw_read_rec(Rn, lane & 7, nxt);
+#endif
     MW_SEG(D, 1);
 
     // the decision of job t against record `x`
@@ -1051,8 +1066,10 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     MW_SEG(D, 4);
     // read record t+1's data after acquiring its ready word (the load above is long done)
     flag = flag_n;
+#if !MW_EARLYREC
     lds_acquire();
     mw_read_rec(Rn, lane & 7, nxt);
+#endif
     MW_SEG(D, 5);
     // bookkeeping: dirty row, bitmap bit — fire-and-forget LDS writes from lane E (the other
     // lanes write their own sink words: no exec masking, no branch)
