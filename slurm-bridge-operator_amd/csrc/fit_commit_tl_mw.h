@@ -31,6 +31,10 @@
 namespace fitgpu {
 
 constexpr int TM_M = 8;   // items per record (> snapshot lag)
+#ifndef TM_LIGHT
+#define TM_LIGHT 0  // 1: the decider's common apply path (an LDS list, staged if new) straight-line,
+                    // slot record written by exec-masked stores; 0: the branchy general path only
+#endif
 #ifndef TM_STAGE2
 #define TM_STAGE2 0  // 1: the helper also stages the record's second clean item's run list — slab
                      // reads of new dirty lists 0.054 -> 0.007 per job, but C5 125.9 -> 129.0 ms
@@ -826,6 +830,54 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         // the list in registers (run `lane`): a new dirty node's from the helper's stage (or the
         // slab), an LDS list's from its region; tm_reserve writes the whole new list
         Seg g{0, 0, 0, 0};
+        int nn = -1;
+        bool light = false;
+#if TM_LIGHT
+        // the common case without branches: an LDS list (a dirty slot's region, or a new dirty
+        // node staged by the helper) that still fits its region after the reservation.  Lane 0
+        // writes the slot record with exec-masked stores (a new node: the whole record and its
+        // bitmap bit; an old one: count and flag).  Anything else falls through to the general
+        // path below (tm_reserve writes nothing when it returns -1).
+        if (__builtin_expect(!glob && (!fresh || (cur.h2.y == pos && (int32_t)cur.h2.z == cnt && cnt <= X.R)), 1)) {
+            const uint32_t la = fresh ? lds_addr(&S->stage[t & (TM_R - 1)][lane])
+                                      : lds_addr(L + min(lane, X.R - 1));
+            const v4i32 x = *(const lds_v4i32*)(uintptr_t)la;
+            g = Seg{x.x, x.y, x.z, x.w};
+            nn = tm_reserve(lds_addr(L), lds_addr(PM), lds_addr(&S->scr[lane]), g, cnt, X.R, start,
+                            start + jd, jc, jm, jg);
+            light = nn >= 0;
+            const uint32_t sa = lds_addr(&S->slot[slot]);
+            const uint32_t rel = pos - X.nb;
+            const uint32_t ba = lds_addr(&X.bitmap[rel >> 5]);
+            const uint32_t bv = 1u << (rel & 31);
+            const v4i32 s0 = v4i32{(int32_t)pos, (int32_t)mask, orig, nn};
+            const v4i32 s1 = v4i32{readlane((int32_t)cur.i1.z, w), readlane((int32_t)cur.i1.w, w),
+                                   readlane((int32_t)cur.i2.x, w), 0};
+            const int32_t zero = 0;
+            // exec masks in SGPR pairs (lane 0 or no lane), built from uniform values
+            const uint32_t lf = (uint32_t)rfl((light && fresh) ? 1 : 0), lo = (uint32_t)rfl((light && !fresh) ? 1 : 0);
+            const uint64_t mf = (uint64_t)lf | ((uint64_t)(uint32_t)rfl(0) << 32);
+            const uint64_t mo = (uint64_t)lo | ((uint64_t)(uint32_t)rfl(0) << 32);
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %[sv], exec\n\t"
+                "s_mov_b64 exec, %[mf]\n\t"
+                "ds_write_b128 %[sa], %[s0]\n\t"
+                "ds_write_b128 %[sa], %[s1] offset:16\n\t"
+                "ds_or_b32 %[ba], %[bv]\n\t"
+                "s_mov_b64 exec, %[mo]\n\t"
+                "ds_write_b32 %[sa], %[nn] offset:12\n\t"
+                "ds_write_b32 %[sa], %[z] offset:28\n\t"
+                "s_mov_b64 exec, %[sv]"
+                : [sv] "=&s"(sv)
+                : [mf] "s"(mf), [mo] "s"(mo), [sa] "v"(sa), [s0] "v"(s0), [s1] "v"(s1), [ba] "v"(ba),
+                  [bv] "v"(bv), [nn] "v"(nn), [z] "v"(zero)
+                : "memory");
+            D.nu += (light && fresh) ? 1 : 0;  // uniform: a select
+            TM_CNT(6, (light && fresh) ? 1 : 0);
+        }
+#endif
+        if (!light) {
         if (fresh) {  // a clean winner becomes dirty slot nu
             glob = cnt > X.R;
             if (!glob) {
@@ -865,7 +917,6 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         a1 = __builtin_amdgcn_s_memtime();
         TM_ADD(3, a1 - a0);
 #endif
-        int nn;
         if (!glob) {
             nn = tm_reserve(lds_addr(L), lds_addr(PM), lds_addr(&S->scr[lane]), g, cnt, X.R, start,
                             start + jd, jc, jm, jg);
@@ -881,6 +932,11 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             nn = tl_reserve_any(X.slab + (int64_t)pos * TL_MAX_SLOTS, cnt, start, start + jd, jc, jm, jg,
                                 S->scr);
         }
+        if (lane == 0) {  // the helpers' view of the slot
+            S->slot[slot].cnt = nn;
+            S->slot[slot].glob = glob ? 1 : 0;
+        }
+        }  // !light
 #else
         if (fresh) {  // a clean winner becomes dirty slot nu: its runs into the slot's LDS region
             glob = cnt > X.R;
@@ -933,11 +989,11 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             nn = tl_reserve_any(X.slab + (int64_t)pos * TL_MAX_SLOTS, cnt, start, start + jd, jc, jm, jg,
                                 S->scr);
         }
-#endif
         if (lane == 0) {  // the helpers' view of the slot
             S->slot[slot].cnt = nn;
             S->slot[slot].glob = glob ? 1 : 0;
         }
+#endif
         cnt = nn;
         {
             TM_CLK(a2);
