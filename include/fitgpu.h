@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 5
+#define FITGPU_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -240,6 +240,14 @@ int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32
  * gpu2-ib), NUL-separated into buf; returns the count, FIT_E_PARSE or FIT_E_INVAL (buf too
  * small).  The fix for parsePartition's split of "Nodes=node[1-3,5]" (parse.go:278-289). */
 int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen);
+/* The Partition RPC's node list (PartitionResponse.nodes, workload.proto; n NUL-separated entries
+ * as parsePartition split them on every comma, parse.go:278-289: "node[1-3" "5]" for
+ * "Nodes=node[1-3,5]") → the expanded node names, NUL-separated into buf, in hostlist order.
+ * These are the names to send to the Nodes RPC (Client.Nodes, slurm.go:343-364, which joins them
+ * with commas for `scontrol show nodes`); record i of its answer is name i, and a caller must
+ * refuse the answer when the record count differs.  Returns the count, FIT_E_PARSE (malformed
+ * hostlist), FIT_E_INVAL (a name listed twice, or buf too small). */
+int fit_node_names(const char* entries, int32_t n, char* buf, int32_t buflen);
 
 /* ---- batched admission (CreatePod's call site) -----------------
  * The virtual kubelet calls CreatePod(ctx, *v1.Pod) (pkg/slurm-virtual-kubelet/provider.go:35-60)
@@ -288,6 +296,44 @@ int fit_admit_group(fit_admitter* a, const fit_admit_req* reqs, int32_t n, fit_a
 int fit_admitter_load_nodes(fit_admitter* a, int32_t n, const int32_t* cpu_free,
                             const int32_t* mem_free, const int32_t* gpu_free,
                             const int32_t* avail_min, const uint32_t* part_mask);
+/* The same with the table's node names and provenance.  names (n NUL-separated, fit_node_names or
+ * fit_ingest_nodes order; NULL = none): open reservations are carried over to the new table by
+ * NAME, so a node added to or removed from the partition does not move them to another node, and
+ * fit_admitter_script can pin a pod to its nodes.  flags FIT_TABLE_STATE: part_mask carries the
+ * nodes' State (fit_ingest_nodes: a DOWN / DRAIN / powered-down node is in no partition), so the
+ * engine never chooses a node slurmctld would refuse, and placements are pinned.  The gRPC Nodes
+ * RPC's Node has no state (workload.proto:165-174): a table built from it marks a drained node
+ * with free capacity schedulable, so by default its placements only gate capacity (the script is
+ * not pinned); FIT_TABLE_PIN pins them anyway (the operator's choice: a pod pinned to a drained
+ * node then pends in Slurm while its reservation holds the capacity, until a TTL or release).
+ * generation: fit_admitter_generation() taken BEFORE the table was fetched (0 = now): a confirmed
+ * reservation is dropped only by a table fetched after its confirmation (earlier tables do not
+ * count the job yet), and a table older than the last one loaded is refused (FIT_E_STATE). */
+#define FIT_TABLE_STATE 1
+#define FIT_TABLE_PIN 2
+typedef struct {
+    int32_t n;
+    const int32_t* cpu_free;
+    const int32_t* mem_free;
+    const int32_t* gpu_free;
+    const int32_t* avail_min;
+    const uint32_t* part_mask;
+    const char* names;
+    int32_t flags;
+    int64_t generation;
+} fit_node_table;
+int fit_admitter_load_table(fit_admitter* a, const fit_node_table* t);
+/* A new table generation (> every earlier one): take it before fetching a table from Slurm. */
+int64_t fit_admitter_generation(fit_admitter* a);
+/* The script to submit for one pod whose admission returned `tickets` (n of them): with
+ * `#SBATCH --nodelist=<names>` (fit_script_with_nodelist) when the pod is one request (n == 1; an
+ * array job's tasks share one sbatch and stay unpinned) and the ticket's nodes come from a named
+ * table loaded with FIT_TABLE_STATE or FIT_TABLE_PIN; the script unchanged otherwise.  *pinned (may be NULL) = 1 when
+ * the directive was added.  The names are those of the table the reservation lives in now, read
+ * under the same lock as placements and reloads.  Returns the length written, FIT_E_INVAL (unknown
+ * ticket, out too small: strlen(script) + 32 + Σ (strlen(name) + 1) suffices). */
+int fit_admitter_script(fit_admitter* a, const int64_t* tickets, int32_t n, const char* script,
+                        char* out, int32_t outlen, int32_t* pinned);
 int fit_admitter_partition_free(fit_admitter* a, int32_t p, int64_t* cpu, int64_t* mem_mib,
                                 int64_t* gpu);
 /* Reservations.  A placed request holds its demand on its nodes from admission until:
@@ -326,6 +372,10 @@ typedef struct {
  * (pkg/slurm-bridge-operator/parse.go:126-135), which gives 0 for "1-10%2" and "1-3,5".
  * FIT_E_PARSE: malformed, or a task id above 4,194,303. */
 int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running);
+/* Slurm's MaxArraySize (slurm.conf, default 1001: task ids 0 .. 1000), which fit_pod_demand
+ * enforces as sbatch does.  1 <= n <= 4,194,304; returns the previous value or FIT_E_INVAL.
+ * Process-wide. */
+int32_t fit_set_max_array_size(int32_t n);
 /* The pod's demand as sbatch sees it: the script's #SBATCH header (extractBatchResourcesFromScript,
  * parse.go:30-69: --time, --nodes, --mem-per-cpu, --cpus-per-task, --ntasks-per-node), overridden
  * by the labels (they reach sbatch as command-line flags, pkg/slurm-agent/slurm.go:189-229; a
@@ -333,7 +383,8 @@ int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running);
  * operator's defaults (pod.go:97-107) and fit_job_demand's per-node rule.  An array job becomes
  * one request per task that may run at once (fit_array_tasks; each task runs on its own nodes).
  * Writes min(n, cap) requests (partition `part`, priority `priority`) and returns n >= 1, or
- * FIT_E_PARSE (malformed #SBATCH header or array) / FIT_E_INVAL (demand out of range). */
+ * FIT_E_PARSE (malformed #SBATCH header or array) / FIT_E_INVAL (demand out of range, or an array
+ * task id >= MaxArraySize: sbatch would refuse the job, fit_set_max_array_size). */
 int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
                    int64_t priority, fit_admit_req* out, int32_t cap);
 /* The script with `#SBATCH --nodelist=<names of node[0..k)>` added as the last line of its

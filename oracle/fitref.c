@@ -507,7 +507,7 @@ static int all_digits(const char* s, size_t n) {
 /* Slurm's --array syntax (sbatch(1) "--array=<indexes>": comma-separated ids and ranges "a-b",
  * ranges with a step "a-b:s", an optional "%N" limit on simultaneously running tasks).  The
  * ids are listed explicitly, sorted and de-duplicated here.  -1: malformed / id > 4194303. */
-int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running) {
+static int array_ids(const char* array, int64_t* tasks, int64_t* running, int64_t* max_id) {
     span a = trim_space(array, strlen(array));
     int64_t limit = -1;
     const char* pct = memchr(a.p, '%', a.n);
@@ -565,12 +565,19 @@ int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running) {
         return -1;
     }
     qsort(ids, cnt, sizeof *ids, cmp_i64);
+    const int64_t ids_max = cnt ? ids[cnt - 1] : -1;
     int64_t distinct = 0;
     for (size_t q = 0; q < cnt; q++) distinct += q == 0 || ids[q] != ids[q - 1];
     free(ids);
     *tasks = distinct;
     *running = (limit > 0 && limit < distinct) ? limit : distinct;
+    *max_id = cnt ? ids_max : -1;
     return 0;
+}
+
+int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running) {
+    int64_t max_id;
+    return array_ids(array, tasks, running, &max_id);
 }
 
 /* One sizecar pod's admission requests: the script's #SBATCH header
@@ -580,8 +587,10 @@ int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running) {
  * pod.go:97-107; ref_job_demand; one request per simultaneously running array task.
  * labels[6] = nodes, cpus-per-task, mem-per-cpu, ntasks-per-node, array, ntask (NULL = absent).
  * out[i*4 + 0..3] = cpu, mem, wall, k for min(n, cap) tasks.  Returns n, or -1 (malformed header
- * or array, the reference's error / panic cases included) / -2 (demand out of range). */
-int ref_pod_demand(const char* const* labels, const char* script, int32_t* out, int cap) {
+ * or array, the reference's error / panic cases included) / -2 (demand out of range, or an array
+ * task id >= max_array_size: Slurm's MaxArraySize, which sbatch enforces). */
+int ref_pod_demand(const char* const* labels, const char* script, int64_t max_array_size,
+                   int32_t* out, int cap) {
     ref_job_resources r;
     memset(&r, 0, sizeof r);
     if (script && ref_extract_batch_resources(script, &r) != 0) return -1;
@@ -595,8 +604,9 @@ int ref_pod_demand(const char* const* labels, const char* script, int32_t* out, 
     int32_t c, m, w;
     uint16_t k;
     if (ref_job_demand(&r, &c, &m, &w, &k) != 0 || k > 8) return -2;
-    int64_t tasks = 1, running = 1;
-    if (labels[4] && labels[4][0] && ref_array_tasks(labels[4], &tasks, &running) != 0) return -1;
+    int64_t tasks = 1, running = 1, max_id = 0;
+    if (labels[4] && labels[4][0] && array_ids(labels[4], &tasks, &running, &max_id) != 0) return -1;
+    if (max_id >= max_array_size) return -2;
     for (int64_t i = 0; i < running && i < cap; i++) {
         out[i * 4 + 0] = c;
         out[i * 4 + 1] = m;

@@ -63,7 +63,8 @@ void ref_pod_request(const ref_job_resources* r, int64_t* cpu, int64_t* memory);
 int ref_job_demand(const ref_job_resources* r, int32_t* cpu, int32_t* mem, int32_t* wall,
                    uint16_t* k);
 int ref_array_tasks(const char* array, int64_t* tasks, int64_t* running);
-int ref_pod_demand(const char* const* labels, const char* script, int32_t* out, int cap);
+int ref_pod_demand(const char* const* labels, const char* script, int64_t max_array_size, int32_t* out,
+                   int cap);
 /* GetPartitionCapacity (pkg/slurm-virtual-kubelet/node.go:169-199). */
 void ref_partition_capacity(const ref_node* nodes, int n, int64_t* cpu, int64_t* memory,
                             int64_t* gpu, int64_t* pods);

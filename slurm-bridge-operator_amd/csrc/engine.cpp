@@ -224,6 +224,7 @@ struct fit_ctx {
     DBuf<int32_t> rb_cpu, rb_mem, rb_gpu;  // fit_read_nodes scratch (col_* stay the loaded table)
     std::vector<uint32_t> h_mask;
     bool have_nodes = false;
+    int64_t loads = 0;        // successful node-table loads (admit.cpp notices a direct load)
 
     // partitions: [max_time | max_cpus | max_mem | comp] × 32
     int32_t np = 0;
@@ -361,6 +362,7 @@ int load_nodes_common(fit_ctx* c, int32_t n) {
     c->n = n;
     c->have_nodes = true;
     c->have_tl = false;  // a timeline belongs to the node table it was built from
+    ++c->loads;
     return 0;
 }
 
@@ -1428,4 +1430,22 @@ int fit_read_timeline(fit_ctx* c, int32_t* cpu, int32_t* mem, int32_t* gpu) {
 
 namespace fitgpu {
 void set_last_error(const char* msg) { g_last_error = msg; }  // admit.cpp: the batch's error
+
+// admit.cpp: the context's table as the admitter's host copy starts from it (a table loaded with
+// fit_load_nodes directly, before the admitter manages it).  Free columns as fit_read_nodes
+// gives them (current, after placements); avail / mask as loaded.
+int64_t ctx_load_count(const fit_ctx* c) { return c && c->have_nodes ? c->loads : 0; }
+int ctx_table(fit_ctx* c, std::vector<int32_t>& cpu, std::vector<int32_t>& mem,
+              std::vector<int32_t>& gpu, std::vector<int32_t>& avail, std::vector<uint32_t>& mask) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (!c->have_nodes) return fail(FIT_E_STATE, "no node table loaded");
+    const size_t m = std::max<int32_t>(c->n, 1);
+    cpu.resize(m), mem.resize(m), gpu.resize(m), avail.resize(m);
+    const int rc = fit_read_nodes(c, cpu.data(), mem.data(), gpu.data());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(avail.data(), c->col_av.p, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost));
+    cpu.resize(c->n), mem.resize(c->n), gpu.resize(c->n), avail.resize(c->n);
+    mask = c->h_mask;
+    return 0;
+}
 }  // namespace fitgpu

@@ -3,6 +3,8 @@
 // behaviour as the Go functions cited on each; one deliberate difference: where the reference
 // panics (a bare flag as the last #SBATCH token, pkg/slurm-bridge-operator/parse.go:58-60) this
 // returns FIT_E_PARSE.  Text is handled as ASCII (scontrol output is ASCII).
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -540,6 +542,28 @@ int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen) {
     return put_names(views, buf, buflen);
 }
 
+int fit_node_names(const char* entries, int32_t n, char* buf, int32_t buflen) {
+    if (n < 0 || (n > 0 && !entries) || !buf || buflen < 0) return FIT_E_INVAL;
+    // parsePartition split the Nodes= value on every comma (parse.go:278-289): joining the pieces
+    // with commas gives the value back, and the hostlist parser splits it at top-level commas only
+    std::string joined;
+    const char* p = entries;
+    for (int32_t i = 0; i < n; ++i, p += strlen(p) + 1) {
+        if (i) joined += ',';
+        joined += p;
+    }
+    std::vector<std::string> names;
+    for (sv item : split_top(trim_space(sv(joined)), ','))
+        if (!item.empty() && !expand_item(item, names)) return FIT_E_PARSE;
+    // one engine row per name: a name listed twice would give `scontrol show nodes` a record count
+    // the table cannot be matched against
+    std::vector<sv> views(names.begin(), names.end());
+    std::vector<sv> sorted(views);
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return FIT_E_INVAL;
+    return put_names(views, buf, buflen);
+}
+
 int fit_ingest_nodes(const char* text, const char* partitions, int32_t np, int32_t cap,
                      int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free, int32_t* avail_min,
                      uint32_t* part_mask, char* names, int32_t names_len) {
@@ -621,83 +645,18 @@ bool array_item(sv it, std::vector<bool>& ids) {
     return true;
 }
 
-// a label value as newSubmitRequestForPod reads it: strconv.ParseInt(v, 10, 64), skipped on error
-int64_t label_int(const char* v) {
-    if (!v) return 0;
-    int64_t x;
-    return parse_int(sv(v), x) == 0 ? x : 0;
-}
-
 }  // namespace
 
-extern "C" {
+namespace fitgpu {
 
-int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running) {
-    if (!array || !tasks || !max_running) return FIT_E_INVAL;
-    sv a = trim_space(sv(array));
-    int64_t limit = INT64_MAX;
-    const size_t pct = a.find('%');
-    if (pct != sv::npos) {
-        const sv l = a.substr(pct + 1);
-        if (l.empty() || l.find_first_not_of("0123456789") != sv::npos || parse_int(l, limit) ||
-            limit < 1)
-            return FIT_E_PARSE;
-        a = a.substr(0, pct);
-    }
-    if (a.empty()) return FIT_E_PARSE;
-    std::vector<bool> ids;
-    for (sv it : split(a, ","))
-        if (!array_item(it, ids)) return FIT_E_PARSE;
-    int64_t n = 0;
-    for (bool b : ids) n += b;
-    *tasks = n;
-    *max_running = n < limit ? n : limit;
-    return FIT_OK;
-}
-
-int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
-                   int64_t priority, fit_admit_req* out, int32_t cap) {
-    if (cap < 0 || (cap > 0 && !out)) return FIT_E_INVAL;
-    fit_pod_labels none{};
-    const fit_pod_labels& L = labels ? *labels : none;
-    fit_job_resources r{};
-    if (script) {
-        const int rc = fit_extract_batch_resources(script, &r);  // parse.go:30-69
-        if (rc) return rc;
-    }
-    // the labels reach sbatch as command-line flags, which override the #SBATCH lines; the array
-    // is counted from the full label (fit_apply_spec keeps 63 characters of it)
-    fit_apply_spec(&r, label_int(L.nodes), label_int(L.cpus_per_task), label_int(L.mem_per_cpu),
-                   label_int(L.ntasks_per_node), nullptr, label_int(L.ntasks));
-    int32_t cpu, mem, wall;
-    uint16_t k;
-    const int rc = fit_job_demand(&r, &cpu, &mem, &wall, &k);
-    if (rc) return rc;
-    if (k > FIT_MAX_K) return FIT_E_INVAL;
-    int64_t tasks = 1, running = 1;
-    if (L.array && L.array[0]) {
-        const int ra = fit_array_tasks(L.array, &tasks, &running);
-        if (ra) return ra;
-    }
-    if (running > INT32_MAX) return FIT_E_INVAL;
-    for (int64_t i = 0; i < running && i < cap; ++i)
-        out[i] = fit_admit_req{priority, cpu, mem, 0, wall, part, k};
-    return (int)running;
-}
-
-int fit_script_with_nodelist(const char* script, const char* names, int32_t n_names,
-                             const int32_t* node, int32_t k, char* out, int32_t outlen) {
-    if (!script || (n_names > 0 && !names) || n_names < 0 || k < 1 || k > FIT_MAX_K || !node ||
-        !out || outlen < 1)
-        return FIT_E_INVAL;
-    std::vector<sv> nm;
-    nm.reserve((size_t)n_names);
-    for (const char* p = names; (int32_t)nm.size() < n_names; p += strlen(p) + 1) nm.push_back(p);
+// The script with `#SBATCH --nodelist=<names>` as the last line of its #SBATCH header
+// (fit_script_with_nodelist, fit_admitter_script).  Length written, or FIT_E_INVAL (out too small).
+int script_with_names(const char* script, const std::vector<std::string_view>& names, char* out,
+                      int32_t outlen) {
     std::string dir = "#SBATCH --nodelist=";
-    for (int32_t i = 0; i < k; ++i) {
-        if (node[i] < 0 || node[i] >= n_names || nm[(size_t)node[i]].empty()) return FIT_E_INVAL;
+    for (size_t i = 0; i < names.size(); ++i) {
         if (i) dir += ',';
-        dir.append(nm[(size_t)node[i]]);
+        dir.append(names[i]);
     }
     dir += '\n';
     // the header: the leading lines extractBatchResourcesFromScript walks (parse.go:36-52) —
@@ -727,10 +686,112 @@ int fit_script_with_nodelist(const char* script, const char* names, int32_t n_na
     if (ins > 0 && s[ins - 1] != '\n') res += '\n';  // a header that ends without a newline
     res += dir;
     res.append(s.substr(ins));
-    if ((int64_t)res.size() + 1 > outlen) return FIT_E_INVAL;
+    if (!out || (int64_t)res.size() + 1 > outlen) return FIT_E_INVAL;
     memcpy(out, res.data(), res.size());
     out[res.size()] = 0;
     return (int)res.size();
+}
+
+}  // namespace fitgpu
+
+namespace {
+
+// a label value as newSubmitRequestForPod reads it: strconv.ParseInt(v, 10, 64), skipped on error
+int64_t label_int(const char* v) {
+    if (!v) return 0;
+    int64_t x;
+    return parse_int(sv(v), x) == 0 ? x : 0;
+}
+
+// Slurm's MaxArraySize (slurm.conf; default 1001): task ids run 0 .. MaxArraySize - 1, and sbatch
+// refuses an --array with a larger id before the job exists
+std::atomic<int32_t> g_max_array_size{1001};
+
+// fit_array_tasks plus the largest task id
+int array_parse(const char* array, int64_t* tasks, int64_t* max_running, int64_t* max_id) {
+    sv a = trim_space(sv(array));
+    int64_t limit = INT64_MAX;
+    const size_t pct = a.find('%');
+    if (pct != sv::npos) {
+        const sv l = a.substr(pct + 1);
+        if (l.empty() || l.find_first_not_of("0123456789") != sv::npos || parse_int(l, limit) ||
+            limit < 1)
+            return FIT_E_PARSE;
+        a = a.substr(0, pct);
+    }
+    if (a.empty()) return FIT_E_PARSE;
+    std::vector<bool> ids;
+    for (sv it : split(a, ","))
+        if (!array_item(it, ids)) return FIT_E_PARSE;
+    int64_t n = 0;
+    for (bool b : ids) n += b;
+    *tasks = n;
+    *max_running = n < limit ? n : limit;
+    *max_id = (int64_t)ids.size() - 1;
+    return FIT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running) {
+    if (!array || !tasks || !max_running) return FIT_E_INVAL;
+    int64_t max_id;
+    return array_parse(array, tasks, max_running, &max_id);
+}
+
+int32_t fit_set_max_array_size(int32_t n) {
+    if (n < 1 || n > (1 << 22)) return FIT_E_INVAL;
+    return g_max_array_size.exchange(n);
+}
+
+int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
+                   int64_t priority, fit_admit_req* out, int32_t cap) {
+    if (cap < 0 || (cap > 0 && !out)) return FIT_E_INVAL;
+    fit_pod_labels none{};
+    const fit_pod_labels& L = labels ? *labels : none;
+    fit_job_resources r{};
+    if (script) {
+        const int rc = fit_extract_batch_resources(script, &r);  // parse.go:30-69
+        if (rc) return rc;
+    }
+    // the labels reach sbatch as command-line flags, which override the #SBATCH lines; the array
+    // is counted from the full label (fit_apply_spec keeps 63 characters of it)
+    fit_apply_spec(&r, label_int(L.nodes), label_int(L.cpus_per_task), label_int(L.mem_per_cpu),
+                   label_int(L.ntasks_per_node), nullptr, label_int(L.ntasks));
+    int32_t cpu, mem, wall;
+    uint16_t k;
+    const int rc = fit_job_demand(&r, &cpu, &mem, &wall, &k);
+    if (rc) return rc;
+    if (k > FIT_MAX_K) return FIT_E_INVAL;
+    int64_t tasks = 1, running = 1, max_id = 0;
+    if (L.array && L.array[0]) {
+        const int ra = array_parse(L.array, &tasks, &running, &max_id);
+        if (ra) return ra;
+    }
+    // sbatch would refuse the array (ids >= MaxArraySize): no request, so one pod's label can
+    // never turn into a batch of millions of tasks
+    if (max_id >= g_max_array_size.load()) return FIT_E_INVAL;
+    for (int64_t i = 0; i < running && i < cap; ++i)
+        out[i] = fit_admit_req{priority, cpu, mem, 0, wall, part, k};
+    return (int)running;
+}
+
+int fit_script_with_nodelist(const char* script, const char* names, int32_t n_names,
+                             const int32_t* node, int32_t k, char* out, int32_t outlen) {
+    if (!script || (n_names > 0 && !names) || n_names < 0 || k < 1 || k > FIT_MAX_K || !node ||
+        !out || outlen < 1)
+        return FIT_E_INVAL;
+    std::vector<sv> nm;
+    nm.reserve((size_t)n_names);
+    for (const char* p = names; (int32_t)nm.size() < n_names; p += strlen(p) + 1) nm.push_back(p);
+    std::vector<sv> picked;
+    for (int32_t i = 0; i < k; ++i) {
+        if (node[i] < 0 || node[i] >= n_names || nm[(size_t)node[i]].empty()) return FIT_E_INVAL;
+        picked.push_back(nm[(size_t)node[i]]);
+    }
+    return fitgpu::script_with_names(script, picked, out, outlen);
 }
 
 int fit_partition_limits(int64_t wall_time_s, int64_t cpu_per_node, int64_t mem_per_node,

@@ -27,9 +27,9 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._lib import (FIT_E_PARSE, FIT_E_STATE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO,
-                   FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64, FIT_XCHG_MAX_I32,
-                   FIT_XCHG_MIN_I32, FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError, FitJobResources,
-                   FitNode, FitOpts, FitPodLabels, FitResources, FitStats, check, lib)
+                   FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, FIT_TABLE_PIN, FIT_TABLE_STATE, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64,
+                   FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32, FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError,
+                   FitJobResources, FitNode, FitNodeTable, FitOpts, FitPodLabels, FitResources, FitStats, check, lib)
 
 __all__ = [
     "Engine", "FitError", "ErrDurationIsUnlimited", "ParseDuration", "parse_resources", "parse_nodes",
@@ -38,7 +38,8 @@ __all__ = [
     "FIT_UNPLACED", "FIT_REJECTED", "Resources", "Node", "JobResources", "TorchHostExchange",
     "FIT_SHARD_AUTO", "FIT_SHARD_NODES", "FIT_SHARD_COMPONENTS", "expand_hostlist", "ingest_nodes",
     "FIT_FLAG_COLLECTIVES", "Admitter", "array_tasks", "pod_demand", "script_with_nodelist",
-    "partition_limits", "node_columns", "POD_LABEL_KEYS",
+    "partition_limits", "node_columns", "POD_LABEL_KEYS", "node_names", "set_max_array_size", "FIT_TABLE_STATE",
+    "FIT_TABLE_PIN",
 ]
 
 
@@ -124,6 +125,23 @@ def expand_hostlist(expr: str) -> list[str]:
             return [x.decode() for x in buf.raw.split(b"\0")[:n]]
         if buflen > 1 << 28:
             check(n, "fit_expand_hostlist")
+        buflen *= 16
+
+
+def node_names(entries: list[str]) -> list[str]:
+    """The Partition RPC's node list (parsePartition's comma split, parse.go:278-289) → the expanded
+    node names to send to the Nodes RPC, one engine row each (fit_node_names)."""
+    blob = b"".join(e.encode() + b"\0" for e in entries)
+    buflen = 1 << 16
+    while True:
+        buf = C.create_string_buffer(buflen)
+        n = lib().fit_node_names(blob, len(entries), buf, buflen)
+        if n == FIT_E_PARSE:
+            raise ValueError(f"malformed hostlist {entries!r}")
+        if n >= 0:
+            return [x.decode() for x in buf.raw.split(b"\0")[:n]]
+        if buflen > 1 << 28:
+            check(n, "fit_node_names")
         buflen *= 16
 
 
@@ -232,6 +250,11 @@ def array_tasks(array: str) -> tuple[int, int]:
         raise ValueError(f"malformed array {array!r}")
     check(rc, "fit_array_tasks")
     return n.value, r.value
+
+
+def set_max_array_size(n: int) -> int:
+    """Slurm's MaxArraySize for pod_demand (process-wide; default 1001); returns the previous one."""
+    return check(lib().fit_set_max_array_size(n), "fit_set_max_array_size")
 
 
 def pod_demand(labels: dict, script: str | None, part: int = 0, priority: int = 0) -> list[tuple]:
@@ -525,6 +548,33 @@ class Admitter:
         check(self._call(lambda h: lib().fit_admitter_load_nodes(h, len(cols[0]), *[_ptr(c) for c in cols])),
               "fit_admitter_load_nodes")
         self._engine.n = len(cols[0])
+
+    def load_table(self, nodes, names: list[str] | None = None, state: bool = False, pin: bool = False,
+                   generation: int = 0):
+        """fit_admitter_load_table: the node table with its names (reservations follow nodes by
+        name; pinning needs them), whether part_mask carries node State (FIT_TABLE_STATE: pinned)
+        and whether to pin without State (FIT_TABLE_PIN)."""
+        cols = [np.ascontiguousarray(nodes.cpu_free, np.int32), np.ascontiguousarray(nodes.mem_free, np.int32),
+                np.ascontiguousarray(nodes.gpu_free, np.int32), np.ascontiguousarray(nodes.avail_min, np.int32),
+                np.ascontiguousarray(nodes.part_mask, np.uint32)]
+        blob = b"".join(x.encode() + b"\0" for x in names) if names is not None else None
+        t = FitNodeTable(len(cols[0]), *[c.ctypes.data for c in cols], blob,
+                         (FIT_TABLE_STATE if state else 0) | (FIT_TABLE_PIN if pin else 0), generation)
+        check(self._call(lambda h: lib().fit_admitter_load_table(h, C.byref(t))), "fit_admitter_load_table")
+        self._engine.n = len(cols[0])
+
+    def generation(self) -> int:
+        return check(self._call(lambda h: lib().fit_admitter_generation(h)), "fit_admitter_generation")
+
+    def script(self, tickets: list[int], script: str) -> tuple[str, bool]:
+        """(script to submit, pinned): fit_admitter_script."""
+        t = (C.c_int64 * len(tickets))(*tickets)
+        outlen = len(script.encode()) + 64 + 4096 * 8
+        buf = C.create_string_buffer(outlen)
+        pinned = C.c_int32()
+        n = check(self._call(lambda h: lib().fit_admitter_script(h, t, len(tickets), script.encode(), buf, outlen,
+                                                                 C.byref(pinned))), "fit_admitter_script")
+        return buf.raw[:n].decode(), bool(pinned.value)
 
     def partition_free(self, p: int):
         c, m, g = C.c_int64(), C.c_int64(), C.c_int64()

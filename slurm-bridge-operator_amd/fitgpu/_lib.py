@@ -38,7 +38,8 @@ EXPORTS = [
     "fit_admitter_partition_free", "fit_admitter_confirm", "fit_admitter_release", "fit_admitter_set_ttl",
     "fit_admitter_reservations", "fit_admitter_pending", "fit_admitter_destroy",
     "fit_array_tasks", "fit_pod_demand", "fit_script_with_nodelist", "fit_partition_limits",
-    "fit_node_columns",
+    "fit_node_columns", "fit_node_names", "fit_admitter_load_table", "fit_admitter_generation",
+    "fit_admitter_script", "fit_set_max_array_size",
 ]
 
 
@@ -80,6 +81,16 @@ class FitAdmitReq(C.Structure):
 class FitAdmitRes(C.Structure):
     _fields_ = [("node", C.c_int32 * FIT_MAX_K), ("batch", C.c_int64), ("batch_jobs", C.c_int32),
                 ("order", C.c_int32), ("ticket", C.c_int64)]
+
+
+FIT_TABLE_STATE = 1  # fit_node_table.flags: part_mask carries node State (include/fitgpu.h)
+FIT_TABLE_PIN = 2    # pin placements on a table without State (the operator's choice)
+
+
+class FitNodeTable(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cpu_free", C.c_void_p), ("mem_free", C.c_void_p), ("gpu_free", C.c_void_p),
+                ("avail_min", C.c_void_p), ("part_mask", C.c_void_p), ("names", C.c_char_p), ("flags", C.c_int32),
+                ("generation", C.c_int64)]
 
 
 class FitPodLabels(C.Structure):
@@ -155,6 +166,13 @@ def lib() -> C.CDLL:
         L.fit_script_with_nodelist.argtypes = [C.c_char_p, C.c_char_p, i32, C.POINTER(i32), i32, C.c_char_p, i32]
         L.fit_partition_limits.argtypes = [i64, i64, i64, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
         L.fit_node_columns.argtypes = [C.POINTER(FitNode), i32, C.c_uint32, P, P, P, P, P]
+        L.fit_node_names.argtypes = [C.c_char_p, i32, C.c_char_p, i32]
+        L.fit_admitter_load_table.argtypes = [P, C.POINTER(FitNodeTable)]
+        L.fit_admitter_generation.argtypes = [P]
+        L.fit_admitter_generation.restype = i64
+        L.fit_admitter_script.argtypes = [P, C.POINTER(i64), i32, C.c_char_p, C.c_char_p, i32, C.POINTER(i32)]
+        L.fit_set_max_array_size.argtypes = [i32]
+        L.fit_set_max_array_size.restype = i32
         L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]
         L.fit_parse_nodes.argtypes = [C.c_char_p, C.POINTER(FitNode), i32]

@@ -1,6 +1,7 @@
 package fitgpu
 
 /*
+#include <stdlib.h>
 #include "fitgpu.h"
 */
 import "C"
@@ -9,6 +10,7 @@ import (
 	"fmt"
 	"runtime"
 	"time"
+	"unsafe"
 )
 
 // Admitter is the cgo binding of fit_admitter (include/fitgpu.h "batched admission"): the
@@ -144,6 +146,79 @@ func (ad *Admitter) LoadNodes(n Nodes) error {
 	}
 	runtime.KeepAlive(ad)
 	return check(rc)
+}
+
+// Table flags (fit_node_table.flags).
+const (
+	// TableState: PartMask carries the nodes' State (IngestNodes: a DOWN / DRAIN node is in no
+	// partition), so placements are pinned with --nodelist.
+	TableState = int32(C.FIT_TABLE_STATE)
+	// TablePin: pin placements on a table without State (the gRPC Nodes RPC's) anyway.
+	TablePin = int32(C.FIT_TABLE_PIN)
+)
+
+// LoadTable replaces the node table with its node names (NodeNames order: reservations follow
+// their node by name across reloads, and Script can pin) and flags (TableState / TablePin).  gen is
+// Generation() taken before the table was fetched from Slurm (0 = now): a table fetched before a
+// Confirm keeps that reservation, a table older than the loaded one is refused.
+func (ad *Admitter) LoadTable(n Nodes, names []string, flags int32, gen int64) error {
+	cnt := len(n.CPUFree)
+	if !sameLen(cnt, len(n.MemFreeMiB), len(n.GPUFree), len(n.AvailMin), len(n.PartMask)) ||
+		(names != nil && len(names) != cnt) {
+		return errLen
+	}
+	t := C.fit_node_table{n: C.int32_t(cnt), flags: C.int32_t(flags), generation: C.int64_t(gen)}
+	var pin runtime.Pinner // the struct holds Go pointers during the call (cgo pointer rules)
+	defer pin.Unpin()
+	if cnt > 0 {
+		for _, p := range []*int32{&n.CPUFree[0], &n.MemFreeMiB[0], &n.GPUFree[0], &n.AvailMin[0]} {
+			pin.Pin(p)
+		}
+		pin.Pin(&n.PartMask[0])
+		t.cpu_free = (*C.int32_t)(unsafe.Pointer(&n.CPUFree[0]))
+		t.mem_free = (*C.int32_t)(unsafe.Pointer(&n.MemFreeMiB[0]))
+		t.gpu_free = (*C.int32_t)(unsafe.Pointer(&n.GPUFree[0]))
+		t.avail_min = (*C.int32_t)(unsafe.Pointer(&n.AvailMin[0]))
+		t.part_mask = (*C.uint32_t)(unsafe.Pointer(&n.PartMask[0]))
+	}
+	if names != nil {
+		cb := C.CBytes(nulJoin(names))
+		defer C.free(cb)
+		t.names = (*C.char)(cb)
+	}
+	rc := C.fit_admitter_load_table(ad.a, &t)
+	runtime.KeepAlive(ad)
+	return check(rc)
+}
+
+// Generation hands out a new table generation; take it before the Nodes RPC of a refresh.
+func (ad *Admitter) Generation() (int64, error) {
+	g := C.fit_admitter_generation(ad.a)
+	runtime.KeepAlive(ad)
+	if g < 0 {
+		return 0, check(C.int(g))
+	}
+	return int64(g), nil
+}
+
+// Script is the sbatch script to submit for a pod admitted with `tickets`: pinned to the
+// reserved nodes with `#SBATCH --nodelist=` when the pod is one request on a named table loaded
+// with TableState or TablePin (fit_admitter_script), unchanged otherwise.
+func (ad *Admitter) Script(tickets []int64, script string) (string, bool, error) {
+	if len(tickets) == 0 {
+		return script, false, nil
+	}
+	sc := C.CString(script)
+	defer C.free(unsafe.Pointer(sc))
+	out := make([]byte, len(script)+64+MaxK*256)
+	var pinned C.int32_t
+	rc := C.fit_admitter_script(ad.a, (*C.int64_t)(unsafe.Pointer(&tickets[0])), C.int32_t(len(tickets)), sc,
+		(*C.char)(unsafe.Pointer(&out[0])), C.int32_t(len(out)), &pinned)
+	runtime.KeepAlive(ad)
+	if err := check(rc); err != nil {
+		return "", false, err
+	}
+	return string(out[:int(rc)]), pinned != 0, nil
 }
 
 // PartitionFree is the allocation-aware free capacity of partition p after the admitted pods.

@@ -298,11 +298,7 @@ func ScriptWithNodelist(script string, names []string, nodes []int32) (string, e
 	if len(nodes) == 0 {
 		return script, nil
 	}
-	blob := make([]byte, 0, 16*len(names)+1)
-	for _, nm := range names {
-		blob = append(append(blob, nm...), 0)
-	}
-	blob = append(blob, 0)
+	blob := nulJoin(names)
 	cb := C.CBytes(blob)
 	defer C.free(cb)
 	sc := C.CString(script)
@@ -315,6 +311,53 @@ func ScriptWithNodelist(script string, names []string, nodes []int32) (string, e
 		return "", err
 	}
 	return string(out[:int(rc)]), nil
+}
+
+func nulJoin(names []string) []byte {
+	blob := make([]byte, 0, 16*len(names)+1)
+	for _, nm := range names {
+		blob = append(append(blob, nm...), 0)
+	}
+	return append(blob, 0)
+}
+
+// NodeNames expands the Partition RPC's node list (parsePartition splits `Nodes=` on every comma,
+// pkg/slurm-agent/parse.go:278-289) into the node names to send to the Nodes RPC: one engine row
+// per name, record i of the answer is name i (fit_node_names).
+func NodeNames(entries []string) ([]string, error) {
+	if len(entries) == 0 {
+		return []string{}, nil
+	}
+	cb := C.CBytes(nulJoin(entries))
+	defer C.free(cb)
+	for size := 1 << 16; ; size *= 16 {
+		buf := make([]byte, size)
+		n := C.fit_node_names((*C.char)(cb), C.int32_t(len(entries)), (*C.char)(unsafe.Pointer(&buf[0])),
+			C.int32_t(size))
+		if n == C.FIT_E_INVAL && size < 1<<24 {
+			continue // buffer too small (or a repeated name: the last try reports it)
+		}
+		if err := check(n); err != nil {
+			return nil, err
+		}
+		out := make([]string, 0, int(n))
+		for b, i := 0, 0; len(out) < int(n); i++ {
+			if buf[i] == 0 {
+				out = append(out, string(buf[b:i]))
+				b = i + 1
+			}
+		}
+		return out, nil
+	}
+}
+
+// SetMaxArraySize sets Slurm's MaxArraySize for PodDemand (process-wide); returns the previous value.
+func SetMaxArraySize(n int32) (int32, error) {
+	rc := C.fit_set_max_array_size(C.int32_t(n))
+	if rc < 0 {
+		return 0, check(C.int(rc))
+	}
+	return int32(rc), nil
 }
 
 // PartitionLimits converts a ResourcesResponse (workload.proto:137-148) into LoadPartitions' limits.

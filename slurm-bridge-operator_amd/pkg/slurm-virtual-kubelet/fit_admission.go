@@ -40,17 +40,22 @@ import (
 
 // FitAdmission holds the engine of one virtual kubelet (one Slurm partition per VK:
 // KubeletServer.SlurmPartition, pkg/configurator/configurator.go:151-171).  The node table is that
-// partition's nodes, in the order of its Partition RPC, every node in partition 0.
+// partition's nodes, one row per name of its expanded Partition RPC list, every node in partition 0.
 type FitAdmission struct {
 	adm     *fitgpu.Admitter
 	eng     *fitgpu.Engine
-	mu      sync.Mutex           // names / tickets
-	names   []string             // node id -> Slurm node name
+	mu      sync.Mutex            // tickets
 	tickets map[types.UID][]int64 // open reservations per pod
+	// PinWithoutState: forward the engine's nodes with --nodelist although the gRPC node table has
+	// no node State (workload.proto:165-174) — a pod pinned to a DOWN / DRAIN node then pends in
+	// Slurm while its reservation holds the capacity.  Default false: the engine gates capacity and
+	// slurmctld picks the nodes.
+	PinWithoutState bool
 }
 
-// NewFitAdmission creates the engine on GPU `device` and loads the partition's limits and nodes.
-func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (*FitAdmission, error) {
+// NewFitAdmission creates the engine on GPU `device` and loads the partition's limits and nodes;
+// pinWithoutState sets FitAdmission.PinWithoutState.
+func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int, pinWithoutState bool) (*FitAdmission, error) {
 	eng, err := fitgpu.New(device)
 	if err != nil {
 		return nil, err // no gfx950 device: the caller keeps the reference behaviour
@@ -75,7 +80,7 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (
 		eng.Close()
 		return nil, err
 	}
-	f := &FitAdmission{adm: adm, eng: eng, tickets: map[types.UID][]int64{}}
+	f := &FitAdmission{adm: adm, eng: eng, tickets: map[types.UID][]int64{}, PinWithoutState: pinWithoutState}
 	if err := f.Refresh(ctx, vk); err != nil {
 		f.Close()
 		return nil, err
@@ -83,16 +88,34 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int) (
 	return f, nil
 }
 
-// Refresh reloads the node table: Partition → Nodes RPCs → fit_node_columns (free = total −
-// alloc per node, workload.proto:165-174).  Open reservations are re-applied by the admitter.
+// Refresh reloads the node table: Partition RPC → fit_node_names (the hostlist parsePartition
+// leaves unexpanded, pkg/slurm-agent/parse.go:278-289) → Nodes RPC for exactly those names →
+// fit_node_columns (free = total − alloc per node, workload.proto:165-174).  Client.Nodes joins the
+// names for one `scontrol show nodes` and returns its records in output order
+// (pkg/slurm-agent/slurm.go:343-364): record i is taken to be name i, and a reply with another
+// record count is refused.  The generation is taken before the RPC, so a confirmation that lands
+// while it is in flight keeps its reservation (the reply does not count that job yet).  Open
+// reservations follow their node by name (fit_admitter_load_table).
 func (f *FitAdmission) Refresh(ctx context.Context, vk *SlurmVirtualKubelet) error {
+	gen, err := f.adm.Generation()
+	if err != nil {
+		return err
+	}
 	pr, err := vk.SlurmClient.Partition(ctx, &workload.PartitionRequest{Partition: vk.KubeletServer.SlurmPartition})
 	if err != nil {
 		return err
 	}
-	nr, err := vk.SlurmClient.Nodes(ctx, &workload.NodesRequest{Nodes: pr.Nodes})
+	names, err := fitgpu.NodeNames(pr.Nodes)
 	if err != nil {
 		return err
+	}
+	nr, err := vk.SlurmClient.Nodes(ctx, &workload.NodesRequest{Nodes: names})
+	if err != nil {
+		return err
+	}
+	if len(nr.Nodes) != len(names) {
+		return fmt.Errorf("fit: partition %s lists %d nodes, scontrol returned %d records",
+			vk.KubeletServer.SlurmPartition, len(names), len(nr.Nodes))
 	}
 	rows := make([]fitgpu.ProtoNode, len(nr.Nodes))
 	for i, n := range nr.Nodes {
@@ -103,13 +126,11 @@ func (f *FitAdmission) Refresh(ctx context.Context, vk *SlurmVirtualKubelet) err
 	if err != nil {
 		return err
 	}
-	f.mu.Lock()
-	defer f.mu.Unlock()
-	if err := f.adm.LoadNodes(t); err != nil {
-		return err
+	flags := int32(0) // no State on this path: capacity gate unless the operator pins anyway
+	if f.PinWithoutState {
+		flags = fitgpu.TablePin
 	}
-	f.names = pr.Nodes
-	return nil
+	return f.adm.LoadTable(t, names, flags, gen)
 }
 
 func (f *FitAdmission) Close() {
@@ -149,21 +170,16 @@ func (f *FitAdmission) admit(pod *v1.Pod) (string, []int64, error) {
 		for i, a := range as {
 			tickets[i] = a.Ticket
 		}
-		if _, isArray := pod.Labels[common.LabelsResourceRequestArray]; isArray {
-			// one sbatch for every task: a --nodelist would pin all of them to every listed node;
-			// the reservations still gate the capacity
-			return script, tickets, nil
-		}
-		f.mu.Lock()
-		names := f.names
-		f.mu.Unlock()
-		pinned, err := fitgpu.ScriptWithNodelist(script, names, as[0].Nodes)
+		// pinned to the reserved nodes when the table allows it (one request, named table with
+		// State or PinWithoutState); an array job's tasks share one sbatch and stay unpinned
+		out, pinned, err := f.adm.Script(tickets, script)
 		if err != nil {
 			f.release(tickets)
 			return "", nil, err
 		}
-		klog.Infof("pod %s/%s fits on %v (batch %d, %d requests)", pod.Namespace, pod.Name, as[0].Nodes, as[0].Batch, as[0].BatchJobs)
-		return pinned, tickets, nil
+		klog.Infof("pod %s/%s fits on %v (batch %d, %d requests, pinned %v)", pod.Namespace, pod.Name,
+			as[0].Nodes, as[0].Batch, as[0].BatchJobs, pinned)
+		return out, tickets, nil
 	case as[0].Nodes[0] == fitgpu.Rejected:
 		return "", nil, fmt.Errorf("pod %s/%s exceeds the partition's limits", pod.Namespace, pod.Name)
 	default: // Unplaced: no node has room now; the library retries the pod

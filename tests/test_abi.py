@@ -12,7 +12,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "fi
 
 def declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|int64_t|const char\*)\s+\**(fit_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t|int64_t|const char\*)\s+\**(fit_\w+)\s*\(", src, re.M)))
 
 
 def test_header_and_binding_agree():
@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.fit_abi_version() == 5
+    assert L.fit_abi_version() == 6
     assert L.fit_strerror(_lib.FIT_E_NODEV) == b"no usable gfx950 device"
 
 

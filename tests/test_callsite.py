@@ -32,14 +32,15 @@ INTS = st.one_of(st.none(), st.integers(-3, 40).map(str), st.sampled_from(["x", 
                                                                            "4096", "3000000000"]))
 ARRAYS = st.one_of(st.none(), st.sampled_from([
     "", "1-4", "0-15", "1,3,5-7", "0-15:4", "1-100%10", "1-10%2", "5", "1-3,5", "x-y", "1-", "-3", "4-1",
-    "1-10:0", "0-4194303%3", "0-4194304", "1%", "%2", "1,,2", "7:2", " 1-3 ", "1-3,2-4"]))
+    "1-10:0", "0-4194303%3", "0-4194304", "1%", "%2", "1,,2", "7:2", " 1-3 ", "1-3,2-4", "0-1000%4", "1000",
+    "1001", "0-1001%2", "5-2000:500"]))
 
 
-def oracle_pod_demand(labels: dict, script):
+def oracle_pod_demand(labels: dict, script, max_array_size: int = 1001):
     raw = [None if labels.get(k) is None else str(labels[k]).encode() for k in KEYS]
     arr = (C.c_char_p * 6)(*raw)
     out = np.zeros(4 * 64, np.int32)
-    n = po.lib().ref_pod_demand(arr, None if script is None else script.encode(),
+    n = po.lib().ref_pod_demand(arr, None if script is None else script.encode(), C.c_int64(max_array_size),
                                 out.ctypes.data_as(C.POINTER(C.c_int32)), 64)
     return n, out.reshape(64, 4)
 
@@ -108,6 +109,60 @@ def test_array_tasks_malformed(expr):
         fitgpu.array_tasks(expr)
     t, r = C.c_int64(), C.c_int64()
     assert po.lib().ref_array_tasks(expr.encode(), C.byref(t), C.byref(r)) == -1
+
+
+def test_pod_demand_max_array_size():
+    """an array label is capped by Slurm's MaxArraySize (ids 0 .. MaxArraySize - 1,
+    default 1001), as sbatch refuses it: one label can no longer become millions of requests."""
+    big = {POD_LABEL_KEYS["array"]: "0-4194303%3"}
+    with pytest.raises(fitgpu.FitError) as ei:
+        fitgpu.pod_demand(big, None)
+    assert ei.value.code == fitgpu._lib.FIT_E_INVAL and oracle_pod_demand({"array": "0-4194303%3"}, None)[0] == -2
+    assert len(fitgpu.pod_demand({POD_LABEL_KEYS["array"]: "0-1000"}, None)) == 1001
+    prev = fitgpu.set_max_array_size(4 << 20)
+    try:
+        assert prev == 1001
+        assert len(fitgpu.pod_demand(big, None)) == 3
+        assert oracle_pod_demand({"array": "0-4194303%3"}, None, 4 << 20)[0] == 3
+        with pytest.raises(fitgpu.FitError):
+            fitgpu.set_max_array_size(0)
+    finally:
+        fitgpu.set_max_array_size(prev)
+
+
+@pytest.mark.parametrize("entries,want", [
+    (["node[1-8]"], [f"node{i}" for i in range(1, 9)]),           # C1's Nodes= (the a3 case)
+    (["node[1-3", "5]"], ["node1", "node2", "node3", "node5"]),   # parsePartition's split of node[1-3,5]
+    (["gpu[01-02]-ib", "cpu7", "x[1-2][3-4]"], ["gpu01-ib", "gpu02-ib", "cpu7", "x13", "x14", "x23", "x24"]),
+    ([], []),
+])
+def test_node_names(entries, want):
+    """the engine's node-name table comes from the Partition RPC's list, expanded
+    (fit_node_names), in the order `scontrol show nodes` is asked for them."""
+    assert fitgpu.node_names(entries) == want
+
+
+def test_node_names_errors():
+    with pytest.raises(fitgpu.FitError):
+        fitgpu.node_names(["a", "a"])  # a repeated name: no 1:1 record match
+    with pytest.raises(fitgpu.FitError):
+        fitgpu.node_names(["n[1-3]", "n2"])
+    with pytest.raises(ValueError):
+        fitgpu.node_names(["n[1-"])
+
+
+def test_node_names_match_c1_records():
+    """The C1 fixtures: Partition RPC → fit_node_names gives exactly the NodeName of every record
+    of `scontrol show nodes`, in record order (cross-checked with fit_ingest_nodes)."""
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    part = open(os.path.join(g, "c1_scontrol_show_partition.txt")).read()
+    nodes = open(os.path.join(g, "c1_scontrol_show_nodes.txt")).read()
+    entries = fitgpu.parse_partition(part.strip())
+    assert entries == ["node[1-8]"]
+    names = fitgpu.node_names(entries)
+    _, ingest_names = fitgpu.ingest_nodes(nodes, ["debug"])
+    assert names == ingest_names and len(fitgpu.parse_nodes(nodes)) == len(names) == 8
 
 
 NAMES = ["node01", "node02", "gpu-a", "gpu-b"]
