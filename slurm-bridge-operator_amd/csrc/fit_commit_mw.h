@@ -48,20 +48,6 @@
 
 namespace fitgpu {
 
-#ifndef MW_DTRIM
-#define MW_DTRIM 1  // 1: compile-time record slot, lane-E-only bookkeeping stores (see mw_decide)
-#endif
-#ifndef MW_EARLYREC
-#define MW_EARLYREC 0  // 1: read record t+1's data with its ready word at the start of step t —
-                       // C3 27.68 vs 27.66 / 27.63 ms, C2 15.46 vs 15.43 (r03z): the mid-step read
-                       // was not exposed; the acquire form is kept
-#endif
-#ifndef MW_STALE_SALU
-#define MW_STALE_SALU 0  // 1: item staleness as one 64-lane compare (item l & 7 vs ring entry l >> 3)
-                         // folded on the SALU — 13 fewer VALU, 16 more SALU per step, but the
-                         // compare's VALU -> SGPR -> SALU hand-off lands on the chain: C3 27.72 ->
-                         // 28.57 ms, C2 15.45 -> 16.00 ms (r03q); 0: eight DPP-rotated XORs
-#endif
 #ifndef MW_ITEMS
 #define MW_ITEMS 8
 #endif
@@ -72,10 +58,7 @@ constexpr int MW_R = 8;                 // record ring; slot t & 7 frees once jo
 #endif
 static_assert(MW_SNAP >= 1 && MW_SNAP <= MW_ITEMS, "a later snapshot only shortens the ring span");
 constexpr int MW_WAVES = SCAN_WAVES;    // 1 decider + MW_H helpers
-#ifndef MW_IDLE4
-#define MW_IDLE4 0  // 1: wave 4 (the decider's SIMD partner) stays idle, six helpers
-#endif
-constexpr int MW_H = MW_WAVES - 1 - MW_IDLE4;  // helpers: waves 1..7 (but 4 with MW_IDLE4)
+constexpr int MW_H = MW_WAVES - 1;  // helpers: waves 1..7
 static_assert(MW_M == 8, "the decider holds one item per lane of its 8-lane ring group");
 static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
@@ -123,8 +106,6 @@ struct alignas(16) MwShared {
     uint32_t pad[7];
     MwRec rec[MW_R];
     MwRow rows[UCAP];
-    MwRow sink_rows[64];   // targets of the decider's lanes that do not write a dirty row
-    uint32_t sink_words[64];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
 };
 
@@ -351,21 +332,6 @@ __device__ __forceinline__ uint32_t wave_min32_l63(uint32_t v) {
     v = dpp_min32<0x142, 0xa>(v);
     return dpp_min32<0x143, 0xc>(v);
 }
-// 64-bit minimum over the wave (uniform): two 32-bit passes
-// (the second pass only when several lanes hold the minimum high word: a uniform branch)
-__device__ __forceinline__ uint64_t wave_min64_2pass(uint64_t v) {
-    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    const uint32_t mh = (uint32_t)__builtin_amdgcn_readlane((int)wave_min32_l63(hi), 63);
-    const uint64_t eq = __ballot(hi == mh);
-    uint32_t ml;
-#ifndef MW_NO_TIESKIP
-    if (__popcll(eq) == 1)
-        ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(eq));
-    else
-#endif
-        ml = (uint32_t)__builtin_amdgcn_readlane((int)wave_min32_l63(hi == mh ? lo : 0xffffffffu), 63);
-    return ((uint64_t)mh << 32) | ml;
-}
 // minimum over the wave, valid in lane 63
 __device__ __forceinline__ uint64_t wave_min64_l63(uint64_t v) {
     v = dpp_min64<0xb1>(v);
@@ -445,9 +411,6 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
 // live job of the window, whose window index the record's header carries; a record whose job
 // index is the window size ends the window.  C3: ~14 % of a component's jobs (the ones nothing
 // fits once the cluster has filled) no longer cost a decider step.
-#ifndef FIT_SKIP_CERT
-#define FIT_SKIP_CERT 1  // 0: every job of the window is live (A/B knob)
-#endif
 struct MwCursor {
     int ct;       // job tile of the cursor
     uint64_t cm;  // live jobs of tile ct not yet taken
@@ -463,7 +426,7 @@ __device__ __forceinline__ bool mw_cursor_tile(const MwTiles& T, const CompPlan&
     ++C.ct;
     const int n = min(SCAN_JOBS, P.w - C.ct * SCAN_JOBS);
     const uint64_t valid = n >= 64 ? ~0ull : (1ull << n) - 1ull;
-    if (FIT_SKIP_CERT && T.feas) {
+    if (T.feas) {
         if (!mw_tile_ready(T, C.ct * SCAN_JOBS, ready, S)) return false;
         const uint64_t f = __hip_atomic_load(gview(T.feas) + C.ct, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
@@ -549,10 +512,6 @@ __device__ __forceinline__ void mw_sort(uint64_t (&q)[N]) {
 }
 
 // Extraction of the record's items: the nmax_ smallest tagged entries, one wave minimum each.
-#ifndef MW_XS
-#define MW_XS 1  // 0: the extraction loop with one wave minimum in SGPRs per item (round-1 design)
-#endif
-#if MW_XS
 // straight-line: each minimum lands in every lane (DPP row minima, then the permlane16 / 32
 // swaps of gfx950), so no VALU -> SGPR -> SALU hand-off or branch sits on the helper's chain;
 // all MW_M rounds run, the ones past nmax_ (or past the last entry) take nothing
@@ -582,19 +541,6 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
             q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
         }                                                                                      \
         n_ = rfl(n_);
-#else
-#define MW_EXTRACT                                                                             \
-        for (; n_ < nmax_; ++n_) {                                                             \
-            const uint64_t best_ = wave_min64_2pass(q_[0]);                                    \
-            if (best_ == KEY_INF) break;                                                       \
-            const bool me_ = q_[0] == best_; /* tagged keys are unique */                      \
-            const uint32_t sv_ = (uint32_t)(n_ + 1) << (4u * ((uint32_t)best_ & 7u));          \
-            sel_ = me_ ? sel_ | sv_ : sel_;                                                    \
-            _Pragma("unroll") for (int e = 0; e + 1 < MW_NE; ++e)                              \
-                q_[e] = me_ ? q_[e + 1] : q_[e];                                               \
-            q_[MW_NE - 1] = me_ ? KEY_INF : q_[MW_NE - 1];                                     \
-        }
-#endif
 
 // Helper h (1..MW_H) pre-resolves records i = h-1, h-1+H, ... (record i: the i-th live job of the
 // window, tj[] its window index).  Loads run two records ahead (keys, job row, bound) and one
@@ -835,7 +781,6 @@ struct MwRing {
     v4i32 a;       // cpu, mem, gpu, avail   (= MwRow's first 16 B)
     v4i32 b;       // mask, pos, orig, job   (= MwRow's last 16 B; job -1: dead)
     int32_t slot;  // dirty slot
-    uint32_t pg;   // MW_STALE_SALU: lane l holds entry (l >> 3)'s position (groups of 8 lanes)
 };
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
@@ -906,24 +851,10 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     __hip_atomic_store(&S->dn, ((uint64_t)(uint32_t)D.nu << 32) | (uint32_t)t, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
     // ready word of record t+1 (relaxed; acquired below, before its data is read)
-#if MW_DTRIM
     // t == E (mod 8) while the window runs (each window starts at t = 0 and every step before an
     // exit advances t by one; after an exit the record read below is never used)
     const MwRec* Rn = &S->rec[(E + 1) & (MW_R - 1)];
-#else
-    const MwRec* Rn = &S->rec[(t + 1) & (MW_R - 1)];
-#endif
     const uint32_t flag_n = lds_ld(&Rn->h.ready);
-#if MW_EARLYREC
-    // record t+1's data right behind its ready word, a whole step before it is used: one wave's
-    // LDS requests are served in order and the helper stores the ready word only after its data
-    // stores have completed (release = lgkmcnt(0) before it), so if this ready word reads t + 2 the
-    // data reads that follow it see the record; if not, job t+1 takes the slow path, which waits
-    // for the word, acquires and reads the record again.  The empty asm keeps the compiler from
-    // hoisting the data reads above the ready word.
-    asm volatile("" ::: "memory");
-    mw_read_rec(Rn, lane & 7, nxt);
-#endif
     MW_SEG(D, 1);
 
     // the decision of job t against record `x`
@@ -946,26 +877,6 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                                     jc, jm, jg, jw, jp);
         const uint64_t rkey = live ? rk0 : KEY_INF;
         const uint32_t ip = x.i0.x;
-#if MW_STALE_SALU
-        // item staleness: its node is in the live ring.  Lane l compares item l & 7 (the record
-        // read puts item l & 7 in lane l) with ring entry l >> 3 (R.pg); the live entries are
-        // the ones decisions [v, t) wrote — the L = t - v lanes before E, cyclically — so their
-        // groups form one rotated byte mask, and OR-folding the 64-bit compare mask down to its
-        // low byte leaves bit i = item i is stale.  (An entry killed by a later write of the same
-        // node lies inside the window too, and so does that later entry: same answer.)
-        bool stale;
-        {
-            const int L = min(t - rfl(v), 7);  // 0..7 (v >= t - 7: the helper's snapshot rule)
-            const uint64_t base = L > 0 ? (~0ull >> (64 - 8 * L)) : 0ull;
-            const int sft = 8 * ((E - L) & 7);
-            const uint64_t lg = sft ? (base << sft) | (base >> (64 - sft)) : base;
-            uint64_t m = __ballot(ip == R.pg) & lg;
-            m |= m >> 32;
-            m |= m >> 16;
-            m |= m >> 8;
-            stale = ((m >> (lane & 7)) & 1ull) != 0ull;
-        }
-#else
         // item staleness: its node is in the live ring.  Lanes 8..15 take a copy of the ring
         // (row_ror:8), so row_ror:k, k = 0..7, shows lane i < 8 every ring entry once.
         const uint32_t P0 = live ? (uint32_t)R.b.y : 0xffffffffu;  // positions are < 2^29
@@ -976,7 +887,6 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                        d4 = dpp_ror_xor<4, false>(P2, ip), d5 = dpp_ror_xor<5, false>(P2, ip),
                        d6 = dpp_ror_xor<6, false>(P2, ip), d7 = dpp_ror_xor<7, false>(P2, ip);
         const bool stale = min(min(min(d0, d1), min(d2, d3)), min(min(d4, d5), min(d6, d7))) == 0u;
-#endif
         const uint64_t ik0 = ((uint64_t)x.i0.y << 32) | ip;
         const uint64_t ikey = (lane < n && !stale) ? ik0 : KEY_INF;
         const bool tr = rkey < ikey;  // this lane's ring row beats its item
@@ -1057,26 +967,19 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     R.a.w = writelane_c<E>(na, R.a.w);
     R.b.x = writelane_c<E>(nk, R.b.x);
     R.b.y = writelane_c<E>(pos, R.b.y);
-#if MW_STALE_SALU
-    R.pg = ((lane >> 3) == E) ? (uint32_t)rfl(pos) : R.pg;
-#endif
     R.b.z = writelane_c<E>(no, R.b.z);
     R.b.w = writelane_c<E>(placed ? t : -1, R.b.w);
     R.slot = writelane_c<E>(slot, R.slot);
     MW_SEG(D, 4);
     // read record t+1's data after acquiring its ready word (the load above is long done)
     flag = flag_n;
-#if !MW_EARLYREC
     lds_acquire();
     mw_read_rec(Rn, lane & 7, nxt);
-#endif
     MW_SEG(D, 5);
-    // bookkeeping: dirty row, bitmap bit — fire-and-forget LDS writes from lane E (the other
-    // lanes write their own sink words: no exec masking, no branch)
-#if MW_DTRIM
-    // lane E alone (exec = its bit, or none when the job is not placed) stores the new row and ORs
-    // the bitmap bit (0 when the node was already dirty): 3 LDS ops of one lane instead of 64
-    // lanes' worth of sink traffic in the LDS pipe the helpers share
+    // bookkeeping: dirty row, bitmap bit — fire-and-forget LDS writes, no branch: lane E alone
+    // (exec = its bit, or none when the job is not placed) stores the new row and ORs the bitmap
+    // bit (0 when the node was already dirty): 3 LDS ops of one lane instead of 64 lanes' worth of
+    // traffic in the LDS pipe the helpers share
     {
         typedef __attribute__((address_space(3))) MwRow* LRow;
         const uint32_t ra = (uint32_t)(uintptr_t)(LRow)&S->rows[slot];
@@ -1098,24 +1001,6 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
             : [m] "s"(m), [ra] "v"(ra), [a] "v"(R.a), [b] "v"(R.b), [ba] "v"(ba), [bv] "v"(bv)
             : "memory");
     }
-#else
-    {
-        const bool me = lane == E && placed;
-        MwRow* dst = me ? &S->rows[slot] : &S->sink_rows[lane];
-        __attribute__((address_space(3))) v4i32* d4 = (__attribute__((address_space(3))) v4i32*)(uintptr_t)dst;
-#ifndef MW_DBG_NOROWS
-        d4[0] = R.a;
-        d4[1] = R.b;
-#endif
-        const uint32_t rel = (uint32_t)pos - (uint32_t)P.nb;
-        const bool setb = me && fresh;
-        uint32_t* bw = setb ? &S->bitmap[rel >> 5] : &S->sink_words[lane];
-#ifndef MW_DBG_NOBITMAP
-        __hip_atomic_fetch_or(bw, setb ? 1u << (rel & 31) : 0u, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-    }
-#endif
     D.nu += fresh;
     D.placed += placed;
     MW_SEG(D, 6);
@@ -1137,9 +1022,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     const CompPlan P = plan_sgpr(Pref);  // by value (see mw_helper)
     MwShared* const S = lds_opaque(Sin);
     const int lane = threadIdx.x & 63;
-#ifndef MW_NO_SETPRIO
     __builtin_amdgcn_s_setprio(3);  // shares its SIMD with a helper wave
-#endif
     MwDec D{0, 0, 0, 0, 0, false};
 #ifdef MW_SEGSTAMP
     for (int i = 0; i < 8; ++i) D.seg[i] = 0;
@@ -1149,7 +1032,6 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     R.a = v4i32{0, 0, 0, 0};
     R.b = v4i32{0, -1, -1, -1};  // dead, position matching no item
     R.slot = -1;
-    R.pg = 0xffffffffu;
     int32_t oq = -1, ov = -1;  // placement of job t parked in lane t & 63, stored 64 at a time
     uint64_t waitcyc = 0;
     MW_CLK(d0);
@@ -1216,7 +1098,7 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
                                                          const uint64_t* __restrict__ bnd,
                                                          const JobRec* __restrict__ wjob,
                                                          int32_t* __restrict__ out, int kmax,
-                                                         MwTiles T = MwTiles{nullptr, 0u, nullptr, nullptr, 0u, 0u, 0u}) {
+                                                         MwTiles T = MwTiles{nullptr, 0u, nullptr, nullptr, 0u, 0u, 0u, nullptr}) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
@@ -1235,10 +1117,8 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
             S->res[2] = r.dirty;
             S->res[3] = r.placed;
         }
-    } else if (!MW_IDLE4) {
+    } else {
         mw_helper(P, S, rec, cand, bnd, wjob, wave, T);  // waves 1.. : helpers 1..MW_H
-    } else if (wave != 4) {
-        mw_helper(P, S, rec, cand, bnd, wjob, wave < 4 ? wave : wave - 1, T);
     }
     __syncthreads();
     const CommitResult r{S->res[0], S->res[1], S->res[2], S->res[3]};

@@ -36,23 +36,8 @@ constexpr int TM_M = 8;   // items per record (> snapshot lag)
                    // itself, prefix minima included; a decider whose winner is that item copies the
                    // prepared list into the new dirty slot instead of running tm_reserve
 #endif
-#ifndef TM_LIGHT
-#define TM_LIGHT 0  // 1: the decider's common apply path (an LDS list, staged if new) straight-line,
-                    // slot record written by exec-masked stores; 0: the branchy general path only
-#endif
-#ifndef TM_STAGE2
-#define TM_STAGE2 0  // 1: the helper also stages the record's second clean item's run list — slab
-                     // reads of new dirty lists 0.054 -> 0.007 per job, but C5 125.9 -> 129.0 ms
-                     // (r03w: the helper's record takes longer, 8 KB less LDS for run lists)
-#endif
 constexpr int TM_R = 8;   // record ring
-#ifndef TL_MW_SOLO
-#define TL_MW_SOLO 0  // 1: wave 4 (the decider's SIMD partner) idles; helpers are waves 1-3, 5-7
-#endif
-#ifndef TL_MW_HELPERS
-#define TL_MW_HELPERS (SCAN_WAVES - 1 - TL_MW_SOLO)
-#endif
-constexpr int TM_H = TL_MW_HELPERS;  // helpers: waves 1..TM_H (the others idle during the commit)
+constexpr int TM_H = SCAN_WAVES - 1;  // helpers: waves 1..7
 static_assert(TM_H >= 1 && TM_H <= SCAN_WAVES - 1, "helpers are waves 1..7");
 static_assert(TL_UCAP == 64, "one dirty slot per lane: ring / slot bit masks are 64 wide");
 constexpr int TM_CPL = TL_KS * TL_SLICES / 64;  // clean candidates per helper lane
@@ -98,9 +83,6 @@ struct alignas(16) TmShared {
     Seg stage[TM_R][64];     // the run list of each record's first clean item
 #if TM_PREP
     int4 stagepm[TM_R][64];  // TM_PREP: its prefix minima (the stage then holds the reserved list)
-#endif
-#if TM_STAGE2
-    Seg stage2[TM_R][64];    // ... and of its second (the first is often written meanwhile)
 #endif
     TmSlot slot[TL_UCAP];
     Seg scr[TL_MAX_SLOTS];   // general-path scratch (tl_reserve_any)
@@ -196,14 +178,6 @@ __device__ __forceinline__ uint64_t tm_fit0(const Seg* L, const int4* PM, int cn
     return fit0 ? tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, pos) : KEY_INF;
 }
 
-#ifndef TM_FAST
-#define TM_FAST 1  // 0: the decider's first form (4-ary ring searches, tl_reserve_lds + tl_pm_build)
-#endif
-#ifndef TM_FIT8
-#define TM_FIT8 1  // ring lists' first run ending at or after d: eight lanes per list over its first
-                   // eight runs (one LDS read, one ballot); 0: 64 lanes per list, one read and one
-                   // ballot per list
-#endif
 
 typedef __attribute__((address_space(3))) v4i32 lds_v4i32;
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
@@ -476,24 +450,6 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
                 spos = (uint32_t)readlane((int32_t)cpos[c], fl);
             }
         }
-#if TM_STAGE2
-        // the record's second clean item: the smallest item index above `first`
-        uint32_t fmin2 = 15u;
-#pragma unroll
-        for (int c = 0; c < TM_CPL; ++c) fmin2 = min(fmin2, (ixc[c] != 0u && ixc[c] != first) ? ixc[c] : 15u);
-        const uint32_t second = wave_min32_all(fmin2);
-        uint32_t spos2 = 0xffffffffu;
-        int fl2 = 0, fc2 = 0;
-#pragma unroll
-        for (int c = TM_CPL - 1; c >= 0; --c) {
-            const uint64_t fm = __ballot(ixc[c] != 0u && ixc[c] == second);
-            if (fm) {
-                fl2 = __builtin_ctzll(fm);
-                fc2 = c;
-                spos2 = (uint32_t)readlane((int32_t)cpos[c], fl2);
-            }
-        }
-#endif
         TlHdr ch[TM_CPL];
 #pragma unroll
         for (int c = 0; c < TM_CPL; ++c) {
@@ -508,10 +464,6 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         }
         const v4i32 sv = *(const GAS v4i32*)(slab + (int64_t)(spos != 0xffffffffu ? spos : nb) * TL_MAX_SLOTS + lane);
         const Seg srun{sv.x, sv.y, sv.z, sv.w};
-#if TM_STAGE2
-        const v4i32 sv2 = *(const GAS v4i32*)(slab + (int64_t)(spos2 != 0xffffffffu ? spos2 : nb) * TL_MAX_SLOTS + lane);
-        const Seg srun2{sv2.x, sv2.y, sv2.z, sv2.w};
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next job's prefetch too (older)
         TmRec* const Rr = &S->rec[t & (TM_R - 1)];
 #pragma unroll
@@ -540,15 +492,8 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
             if (scnt <= R && lane < scnt) S->stage[t & (TM_R - 1)][lane] = srun;
 #endif
         }
-        uint32_t spos2w = 0xffffffffu;
-        int32_t scnt2 = 0;
-#if TM_STAGE2
-        if (spos2 != 0xffffffffu) {
-            scnt2 = readlane(fc2 == 0 ? ch[0].cnt : ch[TM_CPL - 1].cnt, fl2);
-            if (scnt2 <= R && lane < scnt2) S->stage2[t & (TM_R - 1)][lane] = srun2;
-            spos2w = spos2;
-        }
-#endif
+        const uint32_t spos2w = 0xffffffffu;  // header words of a second staged list (none)
+        const int32_t scnt2 = 0;
         if (lane == 0) {
             *reinterpret_cast<v4i32*>(&Rr->h.jc) = v4i32{jc, jm, jg, jd};
             *reinterpret_cast<v4u32*>(&Rr->h.pbit) = v4u32{jp, spos, (uint32_t)scnt, spos2w};
@@ -612,7 +557,7 @@ struct TmDec {
     int t, nu, placed, stop;
     uint64_t gm;  // dirty slots whose list lives in the global slab
     uint32_t rb[TM_R];  // LDS byte address of ring entry i's run-list region (uniform)
-    uint32_t rbv;       // the same per lane: lane l holds rb[l >> 3] (TM_FIT8)
+    uint32_t rbv;       // the same per lane: lane l holds rb[l >> 3]
     bool exit;
 #ifdef FIT_STAMPS
     unsigned long long acc[10];
@@ -657,15 +602,12 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         const bool isg = live && ((D.gm >> (R.slot & 63)) & 1ull);
         const bool ok = live && (R.mask & jp) != 0u && jd <= X.H;
         bool fit0 = false;
-        const int sl = R.slot < 0 ? 0 : R.slot;
-#if TM_FAST
         // ring list i's first run ending at or after jd: run `lane` of all 8 lists (one round
         // trip), a ballot each (a list ends at H >= jd, so the first set bit is a real run), then
         // lane i reads list i's prefix minima there
         uint64_t rk;
         {
             int32_t kk = 0;
-#if TM_FIT8
             // lane l: run l & 7 of ring list l >> 3; lane i < 8 takes the first set bit of byte i
             // (a list shorter than eight runs ends at H >= d, so its byte has a real run set);
             // a live list whose first eight runs all end before d takes the general search below
@@ -673,9 +615,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             const uint64_t m8 = __ballot(e8 >= jd);
             const uint32_t byte = (uint32_t)(m8 >> (8 * (lane & 7))) & 0xffu;
             kk = (int32_t)__builtin_ctz(byte | 0x100u);
-            if (__builtin_expect(__ballot(lane < 8 && ok && !isg && byte == 0u) != 0ull, 0))
-#endif
-            {
+            if (__builtin_expect(__ballot(lane < 8 && ok && !isg && byte == 0u) != 0ull, 0)) {
                 const uint32_t lo = 16u * (uint32_t)min(lane, X.R - 1);
                 int32_t ev[TM_R];
 #pragma unroll
@@ -690,10 +630,6 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             fit0 = ok && !isg && pk.x >= jc && pk.y >= jm && pk.z >= jg;
             rk = fit0 ? tl_key(0, pk.x, pk.y, pk.z, jc, jm, jg, R.pos) : KEY_INF;
         }
-#else
-        const uint64_t rk = tm_fit0(X.lr + sl * X.RS, X.pmr + sl * X.RS, R.cnt, X.R, ok && !isg, jc, jm,
-                                    jg, jd, R.pos, fit0);
-#endif
         d.anywalk = __ballot(ok && !fit0) != 0ull;
         // item staleness: its node is in the live ring (lanes 8..15 hold a copy of the ring, so
         // row_ror:k, k = 0..7, shows lane i < 8 every ring entry once)
@@ -759,9 +695,7 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                 // ring lists on LDS that fail at slot 0: a later start can still win only if the
                 // best so far starts later than 0 — walk them (wave-wide, one list at a time)
                 if (d.anywalk && (bm == KEY_INF || (bm >> 54) > 0)) {
-#ifndef TM_COUNT_SLAB
                     TM_CNT(9, 1);
-#endif
                     const int32_t lim = bm == KEY_INF ? X.H : (int32_t)(bm >> 54);
                     const bool ok = live && !isg && (R.mask & jp) != 0u && jd <= X.H;
                     for (uint64_t m = __ballot(ok) & 0xffull; m; m &= m - 1) {
@@ -847,59 +781,13 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         Seg* const L = X.lr + slot * X.RS;
         int4* const PM = X.pmr + slot * X.RS;
         bool glob = (D.gm >> slot) & 1ull;
-#if TM_FAST
         // the list in registers (run `lane`): a new dirty node's from the helper's stage (or the
         // slab), an LDS list's from its region; tm_reserve writes the whole new list
         Seg g{0, 0, 0, 0};
         int nn = -1;
-        bool light = false;
-#if TM_LIGHT
-        // the common case without branches: an LDS list (a dirty slot's region, or a new dirty
-        // node staged by the helper) that still fits its region after the reservation.  Lane 0
-        // writes the slot record with exec-masked stores (a new node: the whole record and its
-        // bitmap bit; an old one: count and flag).  Anything else falls through to the general
-        // path below (tm_reserve writes nothing when it returns -1).
-        if (__builtin_expect(!glob && (!fresh || (cur.h2.y == pos && (int32_t)cur.h2.z == cnt && cnt <= X.R)), 1)) {
-            const uint32_t la = fresh ? lds_addr(&S->stage[t & (TM_R - 1)][lane])
-                                      : lds_addr(L + min(lane, X.R - 1));
-            const v4i32 x = *(const lds_v4i32*)(uintptr_t)la;
-            g = Seg{x.x, x.y, x.z, x.w};
-            nn = tm_reserve(lds_addr(L), lds_addr(PM), lds_addr(&S->scr[lane]), g, cnt, X.R, start,
-                            start + jd, jc, jm, jg);
-            light = nn >= 0;
-            const uint32_t sa = lds_addr(&S->slot[slot]);
-            const uint32_t rel = pos - X.nb;
-            const uint32_t ba = lds_addr(&X.bitmap[rel >> 5]);
-            const uint32_t bv = 1u << (rel & 31);
-            const v4i32 s0 = v4i32{(int32_t)pos, (int32_t)mask, orig, nn};
-            const v4i32 s1 = v4i32{readlane((int32_t)cur.i1.z, w), readlane((int32_t)cur.i1.w, w),
-                                   readlane((int32_t)cur.i2.x, w), 0};
-            const int32_t zero = 0;
-            // exec masks in SGPR pairs (lane 0 or no lane), built from uniform values
-            const uint32_t lf = (uint32_t)rfl((light && fresh) ? 1 : 0), lo = (uint32_t)rfl((light && !fresh) ? 1 : 0);
-            const uint64_t mf = (uint64_t)lf | ((uint64_t)(uint32_t)rfl(0) << 32);
-            const uint64_t mo = (uint64_t)lo | ((uint64_t)(uint32_t)rfl(0) << 32);
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %[sv], exec\n\t"
-                "s_mov_b64 exec, %[mf]\n\t"
-                "ds_write_b128 %[sa], %[s0]\n\t"
-                "ds_write_b128 %[sa], %[s1] offset:16\n\t"
-                "ds_or_b32 %[ba], %[bv]\n\t"
-                "s_mov_b64 exec, %[mo]\n\t"
-                "ds_write_b32 %[sa], %[nn] offset:12\n\t"
-                "ds_write_b32 %[sa], %[z] offset:28\n\t"
-                "s_mov_b64 exec, %[sv]"
-                : [sv] "=&s"(sv)
-                : [mf] "s"(mf), [mo] "s"(mo), [sa] "v"(sa), [s0] "v"(s0), [s1] "v"(s1), [ba] "v"(ba),
-                  [bv] "v"(bv), [nn] "v"(nn), [z] "v"(zero)
-                : "memory");
-            D.nu += (light && fresh) ? 1 : 0;  // uniform: a select
-            TM_CNT(6, (light && fresh) ? 1 : 0);
-        }
+#if TM_PREP
+        bool prepped = false;  // the helper already reserved this job on the staged list
 #endif
-        if (!light) {
-        bool prepped = false;  // TM_PREP: the helper already reserved this job on the staged list
         if (fresh) {  // a clean winner becomes dirty slot nu
             glob = cnt > X.R;
             if (!glob) {
@@ -919,17 +807,9 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
                     const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
                     g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
 #endif
-#if TM_STAGE2
-                } else if (cur.h2.w == pos && (int32_t)cur.h3.z == cnt) {  // the second staged list
-                    const v4u32 x = lds4(&S->stage2[t & (TM_R - 1)][lane])[0];
-                    g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
-#endif
-                } else {  // neither staged item (both written meanwhile)
+                } else {  // not the staged item (written meanwhile)
                     const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
                     g = Seg{x.x, x.y, x.z, x.w};
-#ifdef TM_COUNT_SLAB  // diagnostic: new dirty lists read from the slab instead of the stage
-                    TM_CNT(9, 1);
-#endif
                 }
             }
             if (lane == 0) {
@@ -980,64 +860,6 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
             S->slot[slot].cnt = nn;
             S->slot[slot].glob = glob ? 1 : 0;
         }
-        }  // !light
-#else
-        if (fresh) {  // a clean winner becomes dirty slot nu: its runs into the slot's LDS region
-            glob = cnt > X.R;
-            if (!glob) {
-                // typed loads on both sides: a plain select of the two pointers becomes one flat
-                // load, which waits on the vector-memory path even for the LDS stage
-                Seg g;
-                if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {  // staged by the helper
-                    const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
-                    g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
-                } else {  // not the record's first clean item (that one was written meanwhile)
-                    const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
-                    g = Seg{x.x, x.y, x.z, x.w};
-                }
-                if (lane < cnt) L[lane] = g;
-                const Seg p = lane < cnt ? g : Seg{0, TL_BIG, TL_BIG, TL_BIG};
-                int32_t vc = p.cpu, vm = p.mem, vg = p.gpu;
-                wave_scan_min3(vc, vm, vg);
-                if (lane < cnt) PM[lane] = make_int4(vc, vm, vg, 0);
-            }
-            if (lane == 0) {
-                const uint32_t rel = pos - X.nb;
-                X.bitmap[rel >> 5] |= 1u << (rel & 31);
-                S->slot[slot] = TmSlot{pos, mask, orig, cnt, readlane((int32_t)cur.i1.z, w),
-                                       readlane((int32_t)cur.i1.w, w), readlane((int32_t)cur.i2.x, w),
-                                       glob ? 1 : 0};
-            }
-            if (glob) D.gm |= 1ull << slot;
-            D.nu += 1;
-            TM_CNT(6, 1);
-        }
-#ifdef FIT_STAMPS_FINE
-        a1 = __builtin_amdgcn_s_memtime();
-        TM_ADD(3, a1 - a0);
-#endif
-        int nn;
-        if (!glob) {
-            nn = tl_reserve_lds(L, cnt, X.R, start, start + jd, jc, jm, jg);
-            if (nn >= 0) {
-                tl_pm_build(L, PM, nn);
-            } else {  // outgrows its LDS region: the list moves to the global slab
-                Seg* gl = X.slab + (int64_t)pos * TL_MAX_SLOTS;
-                if (lane < cnt) gl[lane] = L[lane];
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                nn = tl_reserve_any(gl, cnt, start, start + jd, jc, jm, jg, S->scr);
-                D.gm |= 1ull << slot;
-                glob = true;
-            }
-        } else {
-            nn = tl_reserve_any(X.slab + (int64_t)pos * TL_MAX_SLOTS, cnt, start, start + jd, jc, jm, jg,
-                                S->scr);
-        }
-        if (lane == 0) {  // the helpers' view of the slot
-            S->slot[slot].cnt = nn;
-            S->slot[slot].glob = glob ? 1 : 0;
-        }
-#endif
         cnt = nn;
         {
             TM_CLK(a2);
@@ -1203,9 +1025,8 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
                 S->res[3] = r.placed;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // placements, global-slab lists
-        } else if (TL_MW_SOLO ? wave != 4 : wave <= TM_H) {
-            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob,
-                      TL_MW_SOLO && wave > 4 ? wave - 1 : wave, H, T);
+        } else {
+            tm_helper(P, S, lr, pmr, bitmap, RS, R, slab, hdr, cand, bnd, wjob, wave, H, T);
         }
     } else if (threadIdx.x == 0) {
         S->res[0] = S->res[1] = S->res[2] = S->res[3] = 0;

@@ -10,7 +10,6 @@ namespace fitgpu {
 #define FIT_QCAP_LOG2 16
 #endif
 constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
-constexpr unsigned PCAP = 1u << 12;  // priority ring entries (after the task ring): each round's first tile
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
 constexpr unsigned SPIN_LIMIT = 1u << 25;
 constexpr unsigned long long TASK_EXIT = ~0ull;
@@ -20,10 +19,6 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned pad0[31];
     unsigned q_head;   // tiles claimed by workers
     unsigned pad1[31];
-    unsigned p_tail;   // priority tiles reserved by committers
-    unsigned pad3[31];
-    unsigned p_head;   // priority tiles claimed by workers
-    unsigned pad4[31];
     unsigned finished;  // components done
     unsigned error;     // 1 = watchdog
     unsigned pad2[30];
@@ -84,23 +79,6 @@ __device__ __forceinline__ void engine_publish(EngineCtl* ctl, unsigned long lon
         const unsigned idx = base + i;
         const unsigned tile = from + i / nslice, sl = i % nslice;
         __hip_atomic_store(ring + (idx & (QCAP - 1)), engine_task(idx / QCAP + 1, round, tile, sl, c),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Publish job tile `tile` of component c's window (every block-slice) to the PRIORITY ring: idle
-// workers take these before their next task-ring tile (k_engine_tl, TL_PRIO).
-__device__ __forceinline__ void engine_publish_prio(EngineCtl* ctl, unsigned long long* ring,
-                                                    unsigned tile, unsigned nslice, unsigned round,
-                                                    unsigned c) {
-    const unsigned lane = threadIdx.x & 63u;
-    unsigned base = 0;
-    if (lane == 0)
-        base = __hip_atomic_fetch_add(&ctl->p_tail, nslice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
-    for (unsigned i = lane; i < nslice; i += 64) {
-        const unsigned idx = base + i;
-        __hip_atomic_store(ring + QCAP + (idx & (PCAP - 1)), engine_task(idx / PCAP + 1, round, tile, i, c),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

@@ -286,8 +286,8 @@ size_t engine_lds_bytes(int32_t max_component_nodes) {
 }
 
 size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
-size_t engine_ring_bytes() { return sizeof(unsigned long long) * (QCAP + PCAP); }
-size_t engine_ring_tasks() { return QCAP; }  // task-ring entries (the priority ring follows)
+size_t engine_ring_bytes() { return sizeof(unsigned long long) * QCAP; }
+size_t engine_ring_tasks() { return QCAP; }  // task-ring entries
 
 int engine_blocks_per_cu(size_t lds) {
     int n = 0;

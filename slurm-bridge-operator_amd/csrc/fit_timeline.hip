@@ -60,27 +60,22 @@ __device__ __forceinline__ uint64_t tl_key(int32_t s, int32_t mc, int32_t mm, in
 // Per-lane state of the earliest-start walk over one node's runs.
 struct TlWalk {
     int32_t ra, mc, mm, mg, a;  // start of the current feasible stretch (-1: none), its minima, run start
-    uint64_t key;
     bool live;
-    // TL_KEY_LATE: the first d-slot stretch's start and minima, frozen when it completes; the
-    // key is packed once after the walk (tl_walk_key) instead of at every run
+    // the first d-slot stretch's start and minima, frozen when it completes; the key is packed
+    // once after the walk (tl_walk_key) instead of at every run (C5 129.4 -> 128.1 ms, round 3)
     int32_t kra, kmc, kmm, kmg;
     bool got;
 };
-#ifndef TL_KEY_LATE
-#define TL_KEY_LATE 1  // 0: the key packed at every step and selected (round-2 form)
-#endif
 __device__ __forceinline__ TlWalk tl_walk0(bool live) {
-    return TlWalk{-1, 0, 0, 0, 0, KEY_INF, live, 0, 0, 0, 0, false};
+    return TlWalk{-1, 0, 0, 0, 0, live, 0, 0, 0, 0, false};
 }
 
 // One run: extend / break the feasible stretch; a stretch of d slots gives the key.  A lane
 // stops once every start it could still find is later than `lim` (the start of its cut key).
-#ifndef TL_STEP_BF
-#define TL_STEP_BF 1  // 0: the branchy form below (same walk)
-#endif
-// tl_step on lanes where `vld` holds (a lane's runs past its list's end: vld false, and it stays
-// false for the rest of the walk, so only the key and liveness need the gate)
+// Straight-line: every lane computes the step, only a live lane's key / liveness change (a
+// finished lane's stretch fields are never read again), so lanes that diverge on "fits" cost no
+// exec-mask branches.  `vld` false: a lane's runs past its list's end (it stays false for the
+// rest of the walk, so only the key and liveness need the gate).
 __device__ __forceinline__ void tl_step_v(TlWalk& w, bool vld, int32_t end, int32_t c, int32_t m,
                                           int32_t g, int32_t jc, int32_t jm, int32_t jg, int32_t d,
                                           int32_t H, int32_t lim, uint32_t pos) {
@@ -90,18 +85,12 @@ __device__ __forceinline__ void tl_step_v(TlWalk& w, bool vld, int32_t end, int3
     const int32_t mc = nw ? c : min(w.mc, c), mm = nw ? m : min(w.mm, m), mg = nw ? g : min(w.mg, g);
     const bool done = f & (end - ra >= d);
     const bool kill = f ? (ra > lim) : ((end + d > H) | (end > lim));
-    const bool lv = w.live & vld;
-#if TL_KEY_LATE
-    const bool fin = lv & done;
+    const bool fin = w.live & vld & done;
     w.kra = fin ? ra : w.kra;
     w.kmc = fin ? mc : w.kmc;
     w.kmm = fin ? mm : w.kmm;
     w.kmg = fin ? mg : w.kmg;
     w.got = w.got | fin;
-#else
-    const uint64_t k = tl_key(ra, mc, mm, mg, jc, jm, jg, pos);
-    w.key = (lv & done) ? k : w.key;
-#endif
     w.live = vld ? (w.live & !done & !kill) : w.live;
     w.ra = ra;
     w.mc = mc;
@@ -113,51 +102,13 @@ __device__ __forceinline__ void tl_step_v(TlWalk& w, bool vld, int32_t end, int3
 __device__ __forceinline__ void tl_step(TlWalk& w, int32_t end, int32_t c, int32_t m, int32_t g,
                                         int32_t jc, int32_t jm, int32_t jg, int32_t d, int32_t H,
                                         int32_t lim, uint32_t pos) {
-#if TL_STEP_BF
-    // straight-line form: every lane computes the step, only a live lane's key / liveness change
-    // (a finished lane's stretch fields are never read again), so lanes that diverge on "fits"
-    // cost no exec-mask branches
     tl_step_v(w, true, end, c, m, g, jc, jm, jg, d, H, lim, pos);
-    return;
-#endif
-    if (!w.live) return;
-    if (c >= jc && m >= jm && g >= jg) {
-        if (w.ra < 0) {
-            w.ra = w.a;
-            w.mc = c;
-            w.mm = m;
-            w.mg = g;
-        } else {
-            w.mc = min(w.mc, c);
-            w.mm = min(w.mm, m);
-            w.mg = min(w.mg, g);
-        }
-        if (end - w.ra >= d) {
-            w.key = tl_key(w.ra, w.mc, w.mm, w.mg, jc, jm, jg, pos);
-            w.kra = w.ra;
-            w.kmc = w.mc;
-            w.kmm = w.mm;
-            w.kmg = w.mg;
-            w.got = true;
-            w.live = false;
-        } else if (w.ra > lim) {
-            w.live = false;
-        }
-    } else {
-        w.ra = -1;
-        if (end + d > H || end > lim) w.live = false;  // no (competitive) start left
-    }
-    w.a = end;
 }
 
 // the walk's key (KEY_INF: no window found)
 __device__ __forceinline__ uint64_t tl_walk_key(const TlWalk& w, int32_t jc, int32_t jm,
                                                 int32_t jg, uint32_t pos) {
-#if TL_KEY_LATE
     return w.got ? tl_key(w.kra, w.kmc, w.kmm, w.kmg, jc, jm, jg, pos) : KEY_INF;
-#else
-    return w.key;
-#endif
 }
 
 // Earliest start of a d-slot window whose every run holds (jc, jm, jg), and its key, for `live`
@@ -190,13 +141,8 @@ __device__ __forceinline__ uint64_t tl_eval4(const Seg* sg, int cnt, int cap, bo
 #pragma unroll
         for (int u = 0; u < 4; ++u) g[u] = sg[min(i + u, cap - 1)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#if TL_STEP_BF
+        for (int u = 0; u < 4; ++u)
             tl_step_v(w, i + u < cnt, g[u].end, g[u].cpu, g[u].mem, g[u].gpu, jc, jm, jg, d, H, lim, pos);
-#else
-            if (i + u < cnt) tl_step(w, g[u].end, g[u].cpu, g[u].mem, g[u].gpu, jc, jm, jg, d, H, lim, pos);
-#endif
-        }
     }
     return tl_walk_key(w, jc, jm, jg, pos);
 }
@@ -418,27 +364,12 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-// Inclusive prefix minimum over the 64 lanes (DPP: row shifts, then row broadcasts).
-__device__ __forceinline__ int32_t wave_scan_min(int32_t v) {
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = min(v, __builtin_amdgcn_update_dpp(TL_BIG, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return v;
-}
-
-#ifndef TL_SCAN_FUSED
-#define TL_SCAN_FUSED 1  // 0: three separate scans of a DPP move and a min per level (36 VALU)
-#endif
 // Three independent inclusive min-scans (a run list's cpu / mem / gpu columns), interleaved so
 // that each fused v_min_i32_dpp reads a VGPR written two instructions earlier (the DPP hazard's
 // two wait states, cdna_hip_programming.md) — 18 VALU and one s_nop.  A lane whose DPP source does
 // not exist (row_shr at a row's start) or whose row the row_mask leaves out keeps its value
-// (bound_ctrl not set), i.e. min(v, TL_BIG) = v, as in wave_scan_min.
+// (bound_ctrl not set), i.e. min(v, TL_BIG) = v.
 __device__ __forceinline__ void wave_scan_min3(int32_t& a, int32_t& b, int32_t& c) {
-#if TL_SCAN_FUSED
 #define TL_L3(CTL) "v_min_i32_dpp %0, %0, %0 " CTL "\n\tv_min_i32_dpp %1, %1, %1 " CTL \
                    "\n\tv_min_i32_dpp %2, %2, %2 " CTL "\n\t"
     asm volatile("s_nop 1\n\t"
@@ -450,11 +381,6 @@ __device__ __forceinline__ void wave_scan_min3(int32_t& a, int32_t& b, int32_t& 
                  TL_L3("row_bcast:31 row_mask:0xc bank_mask:0xf")
                  : "+v"(a), "+v"(b), "+v"(c));
 #undef TL_L3
-#else
-    a = wave_scan_min(a);
-    b = wave_scan_min(b);
-    c = wave_scan_min(c);
-#endif
 }
 
 // Prefix minima of an LDS run list (<= 64 runs): PM[i] = min over runs [0, i] per column.
@@ -980,13 +906,6 @@ __global__ __launch_bounds__(64) void k_commit_tl(
     if (threadIdx.x == 0) res[c] = r;
 }
 
-#ifndef TL_PRIO
-#define TL_PRIO 0  // each round's first job tile through the priority ring (fit_engine_ctl.h):
-                   // 1 taken by idle workers only, 2 before any task-ring tile
-#endif
-#ifndef FIT_TL_MW
-#define FIT_TL_MW 1  // 0: the single-wave committer (commit_tl_window) in k_engine_tl too
-#endif
 }  // namespace fitgpu
 #include "fit_commit_tl_mw.h"
 namespace fitgpu {
@@ -1021,12 +940,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         if (MODE == 1 && threadIdx.x == 0)
             __hip_atomic_fetch_add(resident, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // ================================================================ committer
-        // FIT_TL_MW: wave 0 runs the round protocol (publish the window's tiles), then all 8
-        // waves commit it (fit_commit_tl_mw.h: wave 0 decides, waves 1..7 pre-resolve);
-        // otherwise wave 0 alone runs both (commit_tl_window).
+        // wave 0 runs the round protocol (publish the window's tiles), then all 8 waves commit
+        // it (fit_commit_tl_mw.h: wave 0 decides, waves 1..7 pre-resolve)
         __shared__ int s_fail;
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        if (!FIT_TL_MW && wave != 0) return;
         const int c = blockIdx.x;
         const CompState S = cs[c];
         int32_t cursor = S.jstart, win = S.wmin;
@@ -1060,14 +977,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 release_agent();  // plan, bound / counter reset and the last window's run lists
-                // FIT_TL_MW: the first TL_AHEAD job tiles now, the rest by the helpers just in time
-                // (tm_tile_ready); single-wave commit: the whole window up front (a committer wave
-                // publishing tiles as the commit reaches them put the ring stores on the commit
-                // chain: 169.5 -> 175 ms)
-                const unsigned npub = (FIT_TL_MW && TL_AHEAD > 0) ? min(ntj, (unsigned)TL_AHEAD) : ntj;
-                // TL_PRIO: the first tile through the priority ring (the commit waits for it; the
-                // task ring holds other components' tiles published ahead of their need)
-                const unsigned np0 = (TL_PRIO && npub > 0) ? 1u : 0u;
+                // the first TL_AHEAD job tiles now, the rest by the helpers just in time
+                // (tm_tile_ready)
+                const unsigned npub = TL_AHEAD > 0 ? min(ntj, (unsigned)TL_AHEAD) : ntj;
 #ifdef FIT_STAMPS
                 if (lane == 0) {  // before the tasks turn visible: a worker may pick tile 0 at once
                     __hip_atomic_store(&ctl->pub[c], __builtin_amdgcn_s_memrealtime(),
@@ -1075,40 +987,27 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 }
 #endif
-                if (np0) engine_publish_prio(ctl, ring, 0u, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
-                engine_publish(ctl, ring, np0, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
-                if (FIT_TL_MW) {
-                    if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
-                } else {
-                    target += ntj * (unsigned)S.nslice;
-                }
+                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
                 if (f && lane == 0) atomicOr(&ctl->error, 1u);
-                if (FIT_TL_MW) {
-                    acquire_agent();  // run lists written back by this block: CU-wide fresh view
-                    if (lane == 0) s_fail = f;
-                }
+                acquire_agent();  // run lists written back by this block: CU-wide fresh view
+                if (lane == 0) s_fail = f;
                 fail = f;
             }
-            if (FIT_TL_MW) {
-                __syncthreads();
-                if (s_fail) break;  // block-uniform
-            } else if (fail) {
-                break;
-            }
+            __syncthreads();
+            if (s_fail) break;  // block-uniform
             const int64_t t1 = (int64_t)__builtin_amdgcn_s_memrealtime();
             // committed while its tiles are scanned: per-tile readiness inside
             const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
             const CommitResult r =
-                FIT_TL_MW ? commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
-                                                MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
-                                                        TL_AHEAD > 0 ? ring : nullptr, ctl,
-                                                        (unsigned)rounds + 1u, (unsigned)c, ntj})
-                          : commit_tl_window<TL_CAND / 64>(P, c, smem, slab, hdr, cand, 0, 1, bnd, wjob, perm, out,
-                                                outs, H, R, &ctl->tdone[c][0], (unsigned)S.nslice);
+                commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
+                                    MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
+                                            TL_AHEAD > 0 ? ring : nullptr, ctl,
+                                            (unsigned)rounds + 1u, (unsigned)c, ntj, nullptr});
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
             // commit's closing barrier)
-            if (FIT_TL_MW && wave == 0) target += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
+            if (wave == 0) target += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
             if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
             if (r.stop == 3) {
                 fail = true;
@@ -1151,38 +1050,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     for (;;) {
         if (threadIdx.x == 0) {
             unsigned long long task = TASK_EXIT;
-            bool got = false;
-            // TL_PRIO 2: a round's first job tile (the commit waits for it) goes before every
-            // task-ring tile — the task ring holds the other components' tiles published ahead
-            // of their need, so behind them a first tile waited ~120 us (tools/tl_stamps.py)
-            while (TL_PRIO == 2 && !held) {
-                unsigned ph = ld_agent(&ctl->p_head);
-                if (ph >= ld_agent(&ctl->p_tail)) break;
-                if (__hip_atomic_compare_exchange_strong(&ctl->p_head, &ph, ph + 1u, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    const unsigned long long pw = (unsigned long long)(ph / PCAP + 1);
-                    for (unsigned ps = 0;; ++ps) {  // reserved before stored: a short wait
-                        const unsigned long long pg = __hip_atomic_load(
-                            ring + QCAP + (ph & (PCAP - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((pg >> 32) == pw) {
-                            task = pg;
-                            break;
-                        }
-                        if (ps > SPIN_LIMIT) {
-                            atomicOr(&ctl->error, 1u);
-                            break;
-                        }
-                    }
-                    got = true;
-                    break;
-                }
-            }
-            if (!got && !held) {
+            if (!held) {
                 idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 held = true;
             }
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
-            for (unsigned spins = 0; !got; ++spins) {
+            for (unsigned spins = 0;; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1190,31 +1063,6 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     task = g;
                     held = false;
                     break;
-                }
-                // TL_PRIO: while its own tile is not yet published, an idle worker takes a
-                // round's first tile from the priority ring (the claimed index stays held)
-                if (TL_PRIO != 0) {
-                    unsigned ph = ld_agent(&ctl->p_head);
-                    if (ph < ld_agent(&ctl->p_tail)) {
-                        if (__hip_atomic_compare_exchange_strong(&ctl->p_head, &ph, ph + 1u, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                            const unsigned long long pw = (unsigned long long)(ph / PCAP + 1);
-                            for (unsigned ps = 0;; ++ps) {  // reserved before stored: a short wait
-                                const unsigned long long pg = __hip_atomic_load(
-                                    ring + QCAP + (ph & (PCAP - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                if ((pg >> 32) == pw) {
-                                    task = pg;
-                                    break;
-                                }
-                                if (ps > SPIN_LIMIT) {
-                                    atomicOr(&ctl->error, 1u);
-                                    break;
-                                }
-                            }
-                            break;
-                        }
-                        continue;  // another worker took it: look again
-                    }
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
                 if (spins > SPIN_LIMIT) {
@@ -1373,7 +1221,7 @@ hipError_t launch_commit_tl(int ncomp, int epl, size_t lds, hipStream_t st, Seg*
 // apart with R + TL_PAD odd (an even multiple of 16 B puts the lanes' own-list reads on one bank).
 constexpr size_t TL_ENGINE_LDS = 160 * 1024;
 static size_t engine_tl_fixed(int32_t max_component_nodes) {
-    const size_t head = FIT_TL_MW ? tm_fixed_bytes() : sizeof(Seg) * TL_MAX_SLOTS;
+    const size_t head = tm_fixed_bytes();
     return head + (size_t)((max_component_nodes + 31) / 32) * 4;
 }
 int engine_tl_runs(int32_t max_component_nodes) {
