@@ -43,7 +43,10 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU × 4 SI
 PEAK_HBM_GBS = 8000.0
 SCAN_OPS_PER_EVAL = 12    # algorithmic int32 ops per (job, node) fit eval
 SCAN_BYTES_PER_EVAL = 20  # algorithmic node-row bytes per eval (pre-reuse)
-CPU_THREADS = 16          # the GPU box's CPU share for one GPU (OMP_NUM_THREADS there)
+# The GPU box's CPU share for one GPU: the lease runs one GPU's command on 16 cores (OMP_NUM_THREADS
+# is set to 16 there), while nproc / os.cpu_count() count the whole machine's CPUs — so "all host
+# cores" (BASELINE.md:22) is this share, not nproc; cpu_baseline's host object states both.
+CPU_THREADS = int(os.environ.get("OMP_NUM_THREADS") or 16)
 
 
 def commit_bytes_per_job(entries: int) -> int:
@@ -577,7 +580,7 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
     best = max(variants, key=lambda v: v["value"])
     return {"value": best["value"], "unit": "placements/s", "cores": best["cores"], "kind": "port",
             "variant": best["kind"], "sample": best["sample"], "host_cpu": _cpu_model(),
-            "variants": variants}
+            "host": _host_info(threads), "variants": variants}
 
 
 def _components(mask) -> int:
@@ -597,6 +600,30 @@ def _components(mask) -> int:
             ra, rb = find(bits[0]), find(b)
             par[max(ra, rb)] = min(ra, rb)
     return len({find(b) for b in used})
+
+
+def _host_info(threads: int) -> dict:
+    """BASELINE.md:23: nproc, the clock, the threads the multi-core variants used and why."""
+    mhz = []
+    try:
+        mhz = [float(ln.split(":", 1)[1]) for ln in open("/proc/cpuinfo") if ln.startswith("cpu MHz")]
+    except (OSError, ValueError):
+        pass
+    fmax = None
+    try:
+        fmax = int(open("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq").read()) / 1000.0
+    except (OSError, ValueError):
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
+            "cpu_mhz_now_median": round(float(np.median(mhz)), 1) if mhz else None, "cpu_mhz_max": fmax,
+            "threads_used": threads, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "why_threads": "the lease's CPU share for one GPU (OMP_NUM_THREADS on the GPU box); nproc and "
+                           "the affinity mask count the whole machine, whose other cores belong to other "
+                           "GPUs' jobs"}
 
 
 def _cpu_model() -> str:

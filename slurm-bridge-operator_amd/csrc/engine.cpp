@@ -45,6 +45,7 @@ hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, 
                                 int32_t* mem, int32_t* gpu);
 size_t engine_lds_bytes(int32_t max_component_nodes);
 size_t engine_ctl_bytes();
+size_t engine_ctl_error_offset();
 size_t engine_ring_bytes();
 size_t engine_ring_tasks();
 int engine_blocks_per_cu(size_t lds);
@@ -439,9 +440,11 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // a multi-node job needs k keys <= B on one slice: the slice that sets B has ks of them, all
     // clean when the job opens a round, so ks >= kmax keeps every round's first job resolvable
     while (ks_min < kmax) ks_min *= 2;
+    // two sets of per-round buffers (plans, candidates, bounds, job rows) by round parity
+    // (fit_engine_ctl.h): a round starts while the previous round's last tiles are still scanned
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
-        c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
-        c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
+        c->plan.ensure(2 * nc) || c->cand.ensure((size_t)2 * nc * per_comp_cand) ||
+        c->bnd.ensure((size_t)2 * nc * wcap) || c->wjob.ensure((size_t)2 * nc * wcap) ||
         c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
         c->h_err.ensure(4))
         return FIT_E_OOM;
@@ -461,15 +464,18 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.jend = jb[k + 1];
         s.cand_off = (int64_t)i * per_comp_cand;
         s.slot0 = (int32_t)(i * wcap);
+        s.cand_alt = (int64_t)(nc + i) * per_comp_cand;
+        s.slot_alt = (int32_t)((nc + i) * wcap);
+        s.pad = 0;
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
-    // task ring: a committer publishes a round only after all of its previous round's tiles are
-    // done, so at most nc * job tiles * slices tiles are outstanding; the ring must hold them all
-    // (a granule overwritten before its worker read it would be lost)
+    // task ring: a committer publishes a round only after all tiles of the round before last are
+    // done, so at most 2 * nc * job tiles * slices tiles are outstanding; the ring must hold them
+    // all (a granule overwritten before its worker read it would be lost)
     int32_t max_slices = 1;
     for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
-    if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)engine_ring_tasks())
+    if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)engine_ring_tasks())
         return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                     nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     size_t lds = engine_lds_bytes(maxnodes);
@@ -495,8 +501,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
                            hipMemcpyDeviceToHost, st));
-    // error word: EngineCtl::error sits at byte offset 2 * 128 + 4
-    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + engine_ctl_error_offset(), 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->h_err.p[0]) return fail(FIT_E_HIP, "placement engine watchdog tripped (code %u)", c->h_err.p[0]);
     float ms = 0.f;
@@ -745,9 +750,10 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     if (const char* e = getenv("FIT_TL_SLICES")) slices = std::max(1, std::min(atoi(e), TL_SLICES));
     if (const char* e = getenv("FIT_TL_MINSUB")) tl_min_sub = std::max(1, atoi(e));
     const int64_t per_comp_cand = wcap * slices * TL_KS;
+    // two sets of per-round buffers by round parity (see run_persistent)
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
-        c->plan.ensure(nc) || c->cand.ensure((size_t)nc * per_comp_cand) ||
-        c->bnd.ensure((size_t)nc * wcap) || c->wjob.ensure((size_t)nc * wcap) ||
+        c->plan.ensure(2 * nc) || c->cand.ensure((size_t)2 * nc * per_comp_cand) ||
+        c->bnd.ensure((size_t)2 * nc * wcap) || c->wjob.ensure((size_t)2 * nc * wcap) ||
         c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
         c->h_err.ensure(4))
         return FIT_E_OOM;
@@ -764,13 +770,16 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         s.jend = jb[k + 1];
         s.cand_off = (int64_t)i * per_comp_cand;
         s.slot0 = (int32_t)(i * wcap);
+        s.cand_alt = (int64_t)(nc + i) * per_comp_cand;
+        s.slot_alt = (int32_t)((nc + i) * wcap);
+        s.pad = 0;
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
     {  // task ring capacity (see run_persistent)
         int32_t max_slices = 1;
         for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
-        if ((int64_t)nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices >
+        if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices >
             (int64_t)engine_ring_tasks())
             return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                         nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
@@ -834,7 +843,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
                            hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + 2 * 128 + 4, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + engine_ctl_error_offset(), 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->h_err.p[0]) return fail(FIT_E_HIP, "timeline engine watchdog tripped (code %u)", c->h_err.p[0]);
     if (resident_late) return fail(FIT_E_HIP, "timeline engine: committer blocks not resident after 10 s");

@@ -157,7 +157,14 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
 // block-slice but write the plan's KW-entry layout, padded with KEY_INF — an exact (list, bound)
 // pair of K entries, whose insertion network is KW / K times cheaper than the full list's: the
 // tile the commit waits for at every round start arrives sooner.
-template <bool PERSISTENT, int K, int KW = K>
+//
+// STAGE (the persistent engine's first job tile of a round, whose scan the commit waits for): the
+// block first copies its block-slice's node rows into LDS (`stage`, SCAN_WAVES * P.sub rows) with
+// vector loads from all 512 lanes — one memory round trip — and the waves then read the rows from
+// LDS.  The plain path's scalar loads, four rows per wait, pay one round trip per four rows: after
+// the acquire that opens every task the rows come from MALL / HBM, and a lone first tile (nothing
+// else runs on its CU to hide the latency) spent most of its ~19 us waiting (C3).
+template <bool PERSISTENT, int K, int KW = K, bool STAGE = false>
 __device__ __forceinline__ void scan_tile(
     const CompPlan& P, int tile, int s, const NodeRec* __restrict__ rec,
     const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
@@ -165,7 +172,7 @@ __device__ __forceinline__ void scan_tile(
     const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
     const uint16_t* __restrict__ jk, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
     JobRec* __restrict__ wjob, uint64_t (*xk)[K][64],
-    unsigned long long* __restrict__ feas = nullptr) {
+    unsigned long long* __restrict__ feas = nullptr, NodeRec* __restrict__ stage = nullptr) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -191,15 +198,35 @@ __device__ __forceinline__ void scan_tile(
     uint32_t lim = 0xffffffffu;
     const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
     const int n1 = min(P.se, n0 + P.sub);
-    int x = n0;
-    for (; x + 4 <= n1; x += 4) {  // 4 rows per batch: four scalar row loads per wait
-        NodeRec r[4];
+    if constexpr (STAGE) {
+        // the block-slice's rows [a, b) into LDS, 16 B per lane per load, all loads in flight
+        const int a = P.sb + s * SCAN_WAVES * P.sub, b = min(P.se, a + SCAN_WAVES * P.sub);
+        typedef int32_t v4 __attribute__((ext_vector_type(4)));
+        const v4* src = reinterpret_cast<const v4*>(rec + a);
+        v4* dst = reinterpret_cast<v4*>(stage);
+        const int nv = 2 * max(b - a, 0);  // two 16-B halves per 32-B row
+        for (int i = threadIdx.x; i < nv; i += SCAN_WAVES * 64) dst[i] = src[i];
+        __syncthreads();
+        int x = n0;
+        for (; x + 4 <= n1; x += 4) {
+            NodeRec r[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = rec[x + u];
+            for (int u = 0; u < 4; ++u) r[u] = stage[x - a + u];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
+            for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
+        }
+        for (; x < n1; ++x) scan_row(stage[x - a], x, J, key, lim);
+    } else {
+        int x = n0;
+        for (; x + 4 <= n1; x += 4) {  // 4 rows per batch: four scalar row loads per wait
+            NodeRec r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = rec[x + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
+        }
+        for (; x < n1; ++x) scan_row(rec[x], x, J, key, lim);
     }
-    for (; x < n1; ++x) scan_row(rec[x], x, J, key, lim);
 
     // merge tree: waves [h, 2h) hand their lists to waves [0, h)
 #pragma unroll

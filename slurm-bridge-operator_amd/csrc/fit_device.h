@@ -73,10 +73,13 @@ struct alignas(16) CompPlan {
 struct CompState {
     int32_t nb, ne, sb, se, nslice, sub;
     int32_t jstart, jend;  // component job list range
-    int64_t cand_off;      // fixed candidate region of this component
-    int32_t slot0;         // fixed window slot region
+    int64_t cand_off;      // fixed candidate region of this component (even rounds)
+    int32_t slot0;         // fixed window slot region (even rounds)
     int32_t wmin, wmax;
     int32_t ks;            // keys per (job, block-slice) (CompPlan::ks)
+    int64_t cand_alt;      // the same for odd rounds (fit_engine_ctl.h: two buffer sets by parity)
+    int32_t slot_alt;
+    int32_t pad;
 };
 
 struct CompOut {

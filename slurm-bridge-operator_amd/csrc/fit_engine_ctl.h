@@ -7,7 +7,7 @@
 namespace fitgpu {
 
 #ifndef FIT_QCAP_LOG2
-#define FIT_QCAP_LOG2 16
+#define FIT_QCAP_LOG2 17
 #endif
 constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
@@ -22,13 +22,19 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned finished;  // components done
     unsigned error;     // 1 = watchdog
     unsigned pad2[30];
-    unsigned done[32][32];  // per component tiles completed (own 128-B line each)
-    unsigned tdone[32][ENGINE_TILES];  // per component, per window job tile: slices completed
+    // per component (own 128-B line each): [1] the last finished round's tag, [2 + p] scan tiles
+    // completed of the rounds with parity p
+    unsigned done[32][32];
+    // Per-round buffers come in two sets, by round parity p = round & 1 (plans, candidates, bounds,
+    // window job rows, these counters and masks): a new round needs only the tiles of the round
+    // before last (same set) to be complete — long done — instead of waiting for the previous
+    // round's tiles still being scanned after its commit stopped.
+    unsigned tdone[2][32][ENGINE_TILES];  // per parity, component, window job tile: slices completed
     // per component, per window job tile: bit j = job j of the tile has a node that fits it at
     // the round's start state (OR over the block-slices; k_engine).  A job without one is
     // unplaced whatever the round decides before it (node state only shrinks within a
     // placement): the commit skips it (fit_commit_mw.h, "live jobs")
-    unsigned long long tfeas[32][ENGINE_TILES];
+    unsigned long long tfeas[2][32][ENGINE_TILES];
     unsigned long long pub[32];        // FIT_STAMPS: realtime of each component's last publish
 };
 
@@ -37,9 +43,10 @@ __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
 }
 
 // Task word: {epoch:32 | skip:1 | round:12 | tile:7 | slice:6 | component:6}.  done[c][1] holds
-// the round tag of component c's last finished commit: a task of that round is dropped unscanned
-// (it only counts as done) — a round that stops early leaves its later tiles unneeded, and
-// scanning them would delay both the next round's start and other components' tiles.
+// the round tag of component c's last finished commit: a task of that round or an earlier one is
+// dropped unscanned (it only counts as done) — a round that stops early leaves its later tiles
+// unneeded, and scanning them would delay both the next round's start and other components'
+// tiles.  Rounds finish in order, so "earlier" is a 12-bit modular comparison.
 static_assert(ENGINE_TILES <= 128, "7 tile bits");
 __device__ __forceinline__ unsigned task_slice(unsigned long long task) {
     return (unsigned)(task >> 6) & 0x3fu;  // up to 64 block-slices per job
@@ -53,9 +60,12 @@ __device__ __forceinline__ unsigned long long engine_task(unsigned long long epo
 __device__ __forceinline__ unsigned task_tile(unsigned long long task) {
     return (unsigned)(task >> 12) & 0x7fu;
 }
+__device__ __forceinline__ unsigned task_round(unsigned long long task) {
+    return (unsigned)(task >> 19) & 0xfffu;
+}
 __device__ __forceinline__ bool task_dropped(EngineCtl* ctl, unsigned long long task) {
     const unsigned c = (unsigned)task & 63u;
-    return ((unsigned)(task >> 19) & 0xfffu) == (ld_agent(&ctl->done[c][1]) & 0xfffu);
+    return ((ld_agent(&ctl->done[c][1]) - task_round(task)) & 0xfffu) < 0x800u;
 }
 // the committer of component c has finished round `round`: drop what is left of its tiles
 __device__ __forceinline__ void engine_round_finished(EngineCtl* ctl, int c, unsigned round) {
@@ -96,9 +106,10 @@ __device__ __forceinline__ void release_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
 }
 
-// Spin (wave 0 of a committer) until component c has completed `target` scan tiles in total.
-__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, unsigned target) {
-    for (unsigned spins = 0; ld_agent(&ctl->done[c][0]) < target;) {
+// Spin (wave 0 of a committer) until component c has completed `target` scan tiles of the
+// rounds with parity p.
+__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, int p, unsigned target) {
+    for (unsigned spins = 0; ld_agent(&ctl->done[c][2 + p]) < target;) {
         if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) return false;
         __builtin_amdgcn_s_sleep(1);
     }

@@ -32,6 +32,11 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
     return commit_window<MW_EPL>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
 }
 
+// A round's first job tile stages its block-slice's node rows in LDS behind the merge buffer and
+// the task slot (scan_tile STAGE) when they fit: SCAN_WAVES * P.sub <= STAGE_ROWS (C3: 8 x 98).
+constexpr size_t STAGE_OFF = (sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16 + 63) & ~(size_t)63;
+constexpr int STAGE_ROWS = 1024;
+
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
     const CompState* __restrict__ cs, CompOut* __restrict__ co, CompPlan* __restrict__ plans,
@@ -55,10 +60,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         const CompState S = cs[c];
         MwShared* M = reinterpret_cast<MwShared*>(smem);
         int32_t cursor = S.jstart, win = S.wmin;
-        unsigned target = 0;
+        unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         while (cursor < S.jend) {
             const int w = min(win, S.jend - cursor);
+            const unsigned rnd = (unsigned)rounds + 1u;  // task round tag
+            const int par = (int)(rnd & 1u);              // buffer set of this round
             CompPlan P;
             P.nb = S.nb;
             P.ne = S.ne;
@@ -70,8 +77,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             P.jbase = cursor;
             P.w = w;
             P.blk0 = 0;
-            P.cand_off = S.cand_off;
-            P.slot0 = S.slot0;
+            P.cand_off = par ? S.cand_alt : S.cand_off;
+            P.slot0 = par ? S.slot_alt : S.slot0;
             int64_t t0 = 0;
             // a window holding a multi-node job is committed by wave 0 alone (commit_window
             // handles k > 1) after its whole scan; the decider/helper pipeline covers k = 1
@@ -80,15 +87,16 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             P.k0 = multi ? 0 : 1;  // a multi-node job needs k <= KS keys in its first tile
             if (wave == 0) {
                 t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-                // the previous round's tiles (also those past its stop) must all be complete
-                // before their buffers and counters are reused
-                bool fail = !wait_tiles(ctl, c, target);
+                // the tiles of the round before last (this round's buffer set; also those past its
+                // stop) must all be complete before their buffers and counters are reused; the
+                // previous round's may still be in flight, in the other set
+                bool fail = !wait_tiles(ctl, c, par, target[par]);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
-                if (lane == 0) plans[c] = P;
-                for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+                if (lane == 0) plans[2 * c + par] = P;
+                for (int i = lane; i < w; i += 64) bnd[P.slot0 + i] = KEY_INF;
                 for (unsigned i = lane; i < ntj; i += 64) {
-                    __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&ctl->tfeas[c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ctl->tfeas[par][c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 release_agent();  // plan, bound / counter reset and last round's node rows → visible
                 // just-in-time publishing (ENGINE_AHEAD > 0, k = 1 windows): the first
@@ -107,9 +115,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 }
 #endif
-                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
-                if (npub == ntj) target += ntiles;  // else: after the commit (M->pubt)
-                if (multi && !fail) fail = !wait_tiles(ctl, c, target);
+                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                if (npub == ntj) target[par] += ntiles;  // else: after the commit (M->pubt)
+                if (multi && !fail) fail = !wait_tiles(ctl, c, par, target[par]);
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // node rows written by this block: CU-wide view for all waves
                 if (lane == 0) s_fail = fail;
@@ -124,13 +132,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 const bool jit = ENGINE_AHEAD > 0 && M->pubt < ntj;  // block-uniform (before the barrier)
                 R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax,
-                                     MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
-                                             jit ? ring : nullptr, ctl,
-                                             (unsigned)rounds + 1u, (unsigned)c, ntj,
-                                             &ctl->tfeas[c][0]});
+                                     MwTiles{&ctl->tdone[par][c][0], (unsigned)S.nslice,
+                                             jit ? ring : nullptr, ctl, rnd, (unsigned)c, ntj,
+                                             &ctl->tfeas[par][c][0]});
                 // every tile published this round (the committer's and the helpers') must be
-                // complete before the next round reuses the buffers: count them
-                if (jit && wave == 0) target += M->pubt * (unsigned)S.nslice;
+                // complete before a later round reuses its buffer set: count them
+                if (jit && wave == 0) target[par] += M->pubt * (unsigned)S.nslice;
             } else {
                 if (wave == 0) {
                     const CommitResult r0 =
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 R = CommitResult{M->res[0], M->res[1], M->res[2], M->res[3]};
                 __syncthreads();
             }
-            if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
+            if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
             if (R.stop == 3) {  // commit watchdog
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
                 break;
@@ -223,26 +230,33 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         const int c = (int)(task & 63u);
         const int s = (int)task_slice(task);
         const int tile = (int)task_tile(task);
+        const int par = (int)(task_round(task) & 1u);  // the round's buffer set
         if (!skip) {
             if (threadIdx.x == 0) acquire_agent();
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
-            const CompPlan P = plans[c];
+            const CompPlan P = plans[2 * c + par];
 #ifndef FIT_K0
 #define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
 #endif
             switch (P.ks) {  // block-uniform; the host picks one of these (engine.cpp)
 #define SCAN_K(K_)                                                                               \
     case K_:                                                                                      \
-        if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0)                                             \
-            scan_tile<true, (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_), K_>(                       \
-                P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob,         \
-                reinterpret_cast<uint64_t(*)[(FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_)][64]>(smem), \
-                &ctl->tfeas[c][tile]);                                                            \
-        else                                                                                      \
+        if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0) {                                     \
+            constexpr int K0_ = (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_);                        \
+            uint64_t(*xk0)[K0_][64] = reinterpret_cast<uint64_t(*)[K0_][64]>(smem);               \
+            if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                              \
+                scan_tile<true, K0_, K_, true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, \
+                                               jk, cand, bnd, wjob, xk0, &ctl->tfeas[par][c][tile],    \
+                                               reinterpret_cast<NodeRec*>(smem + STAGE_OFF));     \
+            else                                                                                  \
+                scan_tile<true, K0_, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, \
+                                         cand, bnd, wjob, xk0, &ctl->tfeas[par][c][tile]);             \
+        } else {                                                                                  \
             scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand,    \
                                 bnd, wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem),           \
-                                &ctl->tfeas[c][tile]);                                            \
+                                &ctl->tfeas[par][c][tile]);                                            \
+        }                                                                                         \
         break;
                 SCAN_K(16)
                 SCAN_K(8)
@@ -268,12 +282,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         __syncthreads();
         if (threadIdx.x == 0) {
             if (!skip) release_agent();
-            __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();  // task_slot is rewritten by thread 0 next iteration
@@ -281,11 +295,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
 }
 
 size_t engine_lds_bytes(int32_t max_component_nodes) {
-    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16;
+    const size_t scan = STAGE_OFF + sizeof(NodeRec) * STAGE_ROWS;
     return std::max(scan, mw_lds_bytes(max_component_nodes));
 }
 
 size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
+size_t engine_ctl_error_offset() { return offsetof(EngineCtl, error); }
 size_t engine_ring_bytes() { return sizeof(unsigned long long) * QCAP; }
 size_t engine_ring_tasks() { return QCAP; }  // task-ring entries
 

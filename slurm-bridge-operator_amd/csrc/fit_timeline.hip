@@ -218,9 +218,15 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
 // vector loads two nodes ahead (in-order vmcnt, so the wait for node x never waits for x+1);
 // the rare walk past the header's runs reads the slab with scalar loads.  Top-TL_KS lists, bound
 // and the LDS merge tree are k_scan's (fit_common.h).
+// A round's first job tile (the commit waits for it; STAGE in scan_tile_tl) has every header of its
+// block-slice and the runs TL_HEAD .. TL_HEAD + TL_STAGE_RUNS - 1 of every node in LDS: `r8` (that
+// node's staged runs) replaces the slab for them.
+constexpr int TL_STAGE_RUNS = 8;
+template <bool STAGE = false>
 __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec& J, int32_t H,
                                              const Seg* __restrict__ slab, uint64_t (&key)[TL_KS],
-                                             unsigned long long& batches) {
+                                             unsigned long long& batches,
+                                             const Seg* __restrict__ r8 = nullptr) {
     const uint64_t cut = key[TL_KS - 1];
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
     TlWalk w = tl_walk0((h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu &&
@@ -237,8 +243,13 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
             if (!__ballot(w.live)) break;
             ++batches;
             Seg r4[TL_HEAD];
+            if (STAGE && b < TL_HEAD + TL_STAGE_RUNS) {  // uniform
 #pragma unroll
-            for (int i = 0; i < TL_HEAD; ++i) r4[i] = sg[b + i];  // inside the slab (TL_HEAD | 1024)
+                for (int i = 0; i < TL_HEAD; ++i) r4[i] = r8[b - TL_HEAD + i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < TL_HEAD; ++i) r4[i] = sg[b + i];  // inside the slab (TL_HEAD | 1024)
+            }
 #pragma unroll
             for (int i = 0; i < TL_HEAD; ++i)
                 if (b + i < cn)
@@ -252,13 +263,22 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
 
 // One scan tile: SCAN_JOBS window jobs × block-slice s of the component (host-driven k_scan_tl
 // and the persistent k_engine_tl workers).  xk: LDS merge buffer.
+// STAGE (k_engine_tl's first job tile of a round, which the commit waits for; needs
+// SCAN_WAVES * P.sub <= TL_STAGE_NODES): the block first copies its block-slice's headers and every
+// node's runs TL_HEAD .. TL_HEAD + TL_STAGE_RUNS - 1 into LDS with vector loads from all 512 lanes
+// — one memory round trip — instead of streaming them per node two nodes ahead, each long walk
+// another round trip (a lone first tile has nothing on its CU to hide them: ~40 us per task, C5).
+constexpr int TL_STAGE_NODES = 256;
+constexpr size_t TL_STAGE_BYTES = (sizeof(TlHdr) + sizeof(Seg) * TL_STAGE_RUNS) * TL_STAGE_NODES;
+template <bool STAGE = false>
 __device__ __forceinline__ void scan_tile_tl(
     const CompPlan& P, int tile, int s, const Seg* __restrict__ slab,
     const TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
-    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[TL_KS][64]) {
+    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[TL_KS][64],
+    unsigned char* __restrict__ stage = nullptr) {
     if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -286,7 +306,30 @@ __device__ __forceinline__ void scan_tile_tl(
 #if defined(FIT_STAMPS) && !defined(FIT_STAMPS_NOSCAN)
     const unsigned long long sc_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (n0 < n1) {
+    if constexpr (STAGE) {
+        typedef int32_t v4 __attribute__((ext_vector_type(4)));
+        const int a = P.sb + s * SCAN_WAVES * P.sub, b = min(P.se, a + SCAN_WAVES * P.sub);
+        const int nn = max(b - a, 0);
+        TlHdr* const sh = reinterpret_cast<TlHdr*>(stage);
+        Seg* const sr = reinterpret_cast<Seg*>(stage + sizeof(TlHdr) * TL_STAGE_NODES);
+        {  // headers: 6 x 16 B per node; runs TL_HEAD.. of node i: slab row i, TL_STAGE_RUNS x 16 B
+            constexpr int HV = sizeof(TlHdr) / 16;
+            const v4* hs = reinterpret_cast<const v4*>(hdr + a);
+            v4* hd = reinterpret_cast<v4*>(sh);
+            for (int i = threadIdx.x; i < HV * nn; i += SCAN_WAVES * 64) hd[i] = hs[i];
+            for (int i = threadIdx.x; i < TL_STAGE_RUNS * nn; i += SCAN_WAVES * 64) {
+                const int k = i / TL_STAGE_RUNS, r = i - k * TL_STAGE_RUNS;  // inside the slab row
+                const v4 v = *reinterpret_cast<const v4*>(slab + (int64_t)(a + k) * TL_MAX_SLOTS + TL_HEAD + r);
+                *reinterpret_cast<v4*>(sr + i) = v;
+            }
+        }
+        __syncthreads();
+        for (int x = n0; x < n1; ++x) {
+            const TlHdr h = sh[x - a];
+            longn += h.cnt > TL_HEAD;
+            tl_scan_node<true>(h, x, J, H, slab, key, batches, sr + (x - a) * TL_STAGE_RUNS);
+        }
+    } else if (n0 < n1) {
         const int z = tl_vzero();
         TlHdr h0 = hdr[n0 + z], h1 = hdr[min(n0 + 1, n1 - 1) + z];
         for (int x = n0; x < n1; x += 2) {
@@ -922,6 +965,9 @@ namespace fitgpu {
 // per CU when the committer's 160 KB of LDS and its helpers' VGPRs size every block of the launch).
 // A MODE 1 block counts itself into `resident` (host-mapped) so that the host launches the
 // workers only once every committer holds its CU.
+// the worker's LDS: merge buffer, task slot, then the first tile's stage (scan_tile_tl STAGE)
+constexpr size_t TL_STAGE_OFF = (sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16 + 63) & ~(size_t)63;
+
 template <int MODE>
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     EngineCtl* __restrict__ ctl, unsigned long long* __restrict__ ring,
@@ -947,11 +993,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const int c = blockIdx.x;
         const CompState S = cs[c];
         int32_t cursor = S.jstart, win = S.wmin;
-        unsigned target = 0;
+        unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity (fit_engine_ctl.h)
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         bool fail = false;
         while (cursor < S.jend) {
             const int w = min(win, S.jend - cursor);
+            const unsigned rnd = (unsigned)rounds + 1u;  // task round tag
+            const int par = (int)(rnd & 1u);              // buffer set of this round
             CompPlan P;
             P.nb = S.nb;
             P.ne = S.ne;
@@ -963,19 +1011,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             P.jbase = cursor;
             P.w = w;
             P.blk0 = 0;
-            P.cand_off = S.cand_off;
-            P.slot0 = S.slot0;
+            P.cand_off = par ? S.cand_alt : S.cand_off;
+            P.slot0 = par ? S.slot_alt : S.slot0;
             P.k0 = 0;
             const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
             if (wave == 0) {
-                // the previous window's tiles (also those past its stop) must all be complete
-                // before their buffers and counters are reused
-                bool f = !wait_tiles(ctl, c, target);
+                // the tiles of the window before last (this round's buffer set; also those past
+                // its stop) must all be complete before their buffers and counters are reused
+                bool f = !wait_tiles(ctl, c, par, target[par]);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
-                if (lane == 0) plans[c] = P;
-                for (int i = lane; i < w; i += 64) bnd[S.slot0 + i] = KEY_INF;
+                if (lane == 0) plans[2 * c + par] = P;
+                for (int i = lane; i < w; i += 64) bnd[P.slot0 + i] = KEY_INF;
                 for (unsigned i = lane; i < ntj; i += 64)
-                    __hip_atomic_store(&ctl->tdone[c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 release_agent();  // plan, bound / counter reset and the last window's run lists
                 // the first TL_AHEAD job tiles now, the rest by the helpers just in time
                 // (tm_tile_ready)
@@ -987,7 +1035,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 }
 #endif
-                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, (unsigned)rounds + 1u, (unsigned)c);
+                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
                 if (f && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // run lists written back by this block: CU-wide fresh view
@@ -1001,14 +1049,14 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
             const CommitResult r =
                 commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
-                                    MwTiles{&ctl->tdone[c][0], (unsigned)S.nslice,
-                                            TL_AHEAD > 0 ? ring : nullptr, ctl,
-                                            (unsigned)rounds + 1u, (unsigned)c, ntj, nullptr});
+                                    MwTiles{&ctl->tdone[par][c][0], (unsigned)S.nslice,
+                                            TL_AHEAD > 0 ? ring : nullptr, ctl, rnd, (unsigned)c, ntj,
+                                            nullptr});
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
             // commit's closing barrier)
-            if (wave == 0) target += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
-            if (threadIdx.x == 0) engine_round_finished(ctl, c, (unsigned)rounds + 1u);
+            if (wave == 0) target[par] += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
+            if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
             if (r.stop == 3) {
                 fail = true;
                 break;
@@ -1089,13 +1137,18 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const int c = (int)(task & 63u);
         const int s = (int)task_slice(task);
         const int tile = (int)task_tile(task);
+        const int par = (int)(task_round(task) & 1u);  // the round's buffer set
         if (!skip) {
             if (threadIdx.x == 0) acquire_agent();
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
-            const CompPlan P = plans[c];
-            scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, H,
-                         slot_min, xk);
+            const CompPlan P = plans[2 * c + par];
+            if (tile == 0 && SCAN_WAVES * P.sub <= TL_STAGE_NODES)  // block-uniform
+                scan_tile_tl<true>(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd,
+                                   wjob, H, slot_min, xk, smem + TL_STAGE_OFF);
+            else
+                scan_tile_tl(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob,
+                             H, slot_min, xk);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
 #ifdef FIT_STAMPS
             if (threadIdx.x == 0 && tile == 0) {  // a round's first tile: pickup delay, scan time
@@ -1111,12 +1164,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         __syncthreads();
         if (threadIdx.x == 0) {
             if (!skip) release_agent();
-            __hip_atomic_fetch_add(&ctl->tdone[c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&ctl->done[c][0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();  // task_slot is rewritten by thread 0 next iteration
@@ -1234,12 +1287,13 @@ int engine_tl_runs(int32_t max_component_nodes) {
     return r;
 }
 
+size_t engine_tl_scan_lds_bytes() { return TL_STAGE_OFF + TL_STAGE_BYTES; }
+
 size_t engine_tl_lds_bytes(int32_t max_component_nodes) {
     const int runs = engine_tl_runs(max_component_nodes);
     const size_t commit = engine_tl_fixed(max_component_nodes) +
                           (sizeof(Seg) + sizeof(int4)) * (size_t)TL_UCAP * (runs > 0 ? runs + TL_PAD : 0);
-    const size_t scan = sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16;
-    return std::max(commit, scan);
+    return std::max(commit, engine_tl_scan_lds_bytes());
 }
 
 int engine_tl_blocks_per_cu(size_t lds, int mode) {
@@ -1250,7 +1304,6 @@ int engine_tl_blocks_per_cu(size_t lds, int mode) {
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_engine_tl<0>, SCAN_WAVES * 64, lds);
     return e == hipSuccess ? n : 0;
 }
-size_t engine_tl_scan_lds_bytes() { return sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16; }
 
 hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
                             const void* cs, void* co, CompPlan* plans, int ncomp, Seg* slab,
