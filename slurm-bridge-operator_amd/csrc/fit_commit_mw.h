@@ -118,7 +118,9 @@ __host__ __device__ constexpr size_t mw_lds_bytes(int32_t max_component_nodes) {
 // [3] helper cycles (sum), [4] helper wait-for-snapshot, [5] helper jobs, [6] items written,
 // [7] (unused), [8] (unused), [9] decider waits in each round's first 8 jobs,
 // [10..12] first-tile scan (workers), [13] helper tile waits, [14] helper snapshot → record,
-// [15] helper snapshot → extraction start, [16] decider: records not ready at the first read
+// [15] helper snapshot → extraction start, [16] committer: round end → tiles published (wait for
+// the round before last, resets, release, publish), [17] decider: start → record 0 ready,
+// [18] rounds
 constexpr int MW_NSTAMP = 24;
 __device__ unsigned long long g_mw[64][MW_NSTAMP];
 #define MW_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -1057,6 +1059,11 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
         mw_read_rec(&S->rec[0], lane & 7, ra);
     } else {
         D.exit = true;
+    }
+    {
+        MW_CLK(r0c);
+        MW_ADD(17, r0c - d0);
+        MW_ADD(18, 1);
     }
     // 8-way unrolled: the ring lane (t & 7) is a constant in every step; the two record register
     // sets alternate with the step's parity; the exit is tested once per 8 steps

@@ -85,6 +85,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // windows and starts at once: helpers wait per job tile (MwTiles)
             const bool multi = jpk[cursor + w] != jpk[cursor];
             P.k0 = multi ? 0 : 1;  // a multi-node job needs k <= KS keys in its first tile
+            MW_CLK(rs0);
             if (wave == 0) {
                 t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                 // the tiles of the round before last (this round's buffer set; also those past its
@@ -121,6 +122,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // node rows written by this block: CU-wide view for all waves
                 if (lane == 0) s_fail = fail;
+                {
+                    MW_CLK(rs1);
+                    MW_ADD(16, rs1 - rs0);
+                }
             }
             __syncthreads();
             if (s_fail) break;  // block-uniform

@@ -147,9 +147,9 @@ def test_groups_in_one_batch_match_oracle():
     def req(prio, cpu, wall=10, n=1, k=1):
         return [(prio, cpu, 1000, 0, wall, 0, k)] * n
 
-    units = [req(0, 40), req(1, 60, n=10),      # 7 of the 10 tasks fit: dropped
+    units = [req(0, 40), req(1, 60, n=10),      # 7 of the 10 tasks would fit: dropped
              req(2, 30), req(3, 20, n=3), req(4, 64), req(5, 100, n=2),   # too big: unplaced, not partial
-             req(6, 50, n=5), req(7, 10), req(8, 14, n=6),                # 5 of 6 fit: dropped
+             req(6, 50, n=5), req(7, 10), req(8, 14, n=6),                # 4 of 5 would fit: dropped
              req(9, 14), req(10, 5, wall=700, n=2),                       # MaxTime 600: rejected
              req(11, 8, k=2), req(12, 2, n=4, k=2), req(13, 3)]
     total = sum(len(u) for u in units)
@@ -174,8 +174,20 @@ def test_groups_in_one_batch_match_oracle():
     assert len({r[0][1] for r in res}) == 1 and res[0][0][2] == total  # one batch
     want, fin = _oracle_units(nodes, parts, units)
     assert [[g[0] for g in r] for r in res] == want
-    assert want[1] == [[FIT_UNPLACED]] * 10 and want[8] == [[FIT_UNPLACED]] * 6
-    assert want[10] == [[FIT_REJECTED]] * 2 and want[2] != [[FIT_UNPLACED]]
+    # the scenario exercises the drop: units 1 and 6 would be placed in part on the table they
+    # meet (so a single fit_place gives them nodes), yet take nothing; unit 5 fits nowhere at all
+    partial = []
+    cur = synth.Nodes(nodes.cpu_free.copy(), nodes.mem_free.copy(), nodes.gpu_free.copy(), nodes.avail_min,
+                      nodes.part_mask)
+    for u, w in zip(units, want):
+        ref, _, f = po.ref_place(cur, _jobs(u), parts, kmax=8)
+        partial.append(0 < int((ref[:, 0] >= 0).sum()) < len(u))
+        if w[0][0] >= 0:
+            cur = synth.Nodes(f[0], f[1], f[2], nodes.avail_min, nodes.part_mask)
+    assert [i for i, x in enumerate(partial) if x] == [1, 6]
+    assert want[1] == [[FIT_UNPLACED]] * 10 and want[6] == [[FIT_UNPLACED]] * 5
+    assert want[5] == [[FIT_UNPLACED]] * 2 and want[10] == [[FIT_REJECTED]] * 2
+    assert want[2] == [[1]]  # the 30-cpu pod behind the dropped group uses the room it left
     assert free == {"cpu": int(np.maximum(fin.cpu_free, 0).sum()), "mem_mib": int(np.maximum(fin.mem_free, 0).sum()),
                     "gpu": 0}
     # order: each request's index in the batch's priority order

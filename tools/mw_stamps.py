@@ -28,6 +28,9 @@ print(f"round's first tile: pickup delay {sum(buf[c * W + 10] for c in range(64)
       f"scan {sum(buf[c * W + 12] for c in range(64)) / t0n / 100:.1f} us (per task, {t0n} tasks)")
 print(f"helpers: tile waits {tot[13] / hj:.0f} cyc/job, snapshot -> record {tot[14] / hj:.0f} cyc/job "
       f"(of which snapshot -> extraction start {tot[15] / hj:.0f})")
+rn = max(tot[18], 1)
+print(f"round start: round end -> tiles published {tot[16] / rn:.0f} cyc, decider start -> record 0 "
+      f"{tot[17] / rn:.0f} cyc (per round, {tot[18]} rounds over all components)")
 print(f"helpers: {tot[3] / hj:.0f} cyc/job (per helper), waiting for snapshot {tot[4] / hj:.0f}, "
       f"items/job {tot[6] / hj:.2f}")
 for c in range(64):
