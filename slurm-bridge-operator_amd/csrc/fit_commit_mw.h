@@ -209,6 +209,30 @@ __device__ __forceinline__ JobRec ld_job(const GAS JobRec* p) {
     return r;
 }
 
+// Write-through reads of a scan tile's outputs (candidates, bound, job row), which the scan workers
+// store through (sc1) and count with an agent-scope add: a helper that has seen the tile's count
+// reach its target in a relaxed agent poll reads them with sc1 loads, which bypass this CU's L1,
+// instead of an acquire fence (≈1.7 us, once per tile per helper, and on every round's start:
+// cdna_hip_programming.md §6 Guideline 16; MI355X_MICROARCH.md hand-off table, row 1 — one block
+// per CU, 8-B sc1 stores and loads, the polling wave loads after its poll matched).
+__device__ __forceinline__ uint64_t ld_through(const GAS uint64_t* p) {
+    return __hip_atomic_load(const_cast<GAS uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ JobRec ld_job_through(const GAS JobRec* p) {
+    const GAS uint64_t* q = (const GAS uint64_t*)p;
+    const uint64_t w0 = ld_through(q), w1 = ld_through(q + 1), w2 = ld_through(q + 2), w3 = ld_through(q + 3);
+    JobRec r;
+    r.q = (int32_t)(uint32_t)w0;
+    r.cpu = (int32_t)(uint32_t)(w0 >> 32);
+    r.mem = (int32_t)(uint32_t)w1;
+    r.gpu = (int32_t)(uint32_t)(w1 >> 32);
+    r.wall = (int32_t)(uint32_t)w2;
+    r.pbit = (uint32_t)(w2 >> 32);
+    r.k = (int32_t)(uint32_t)w3;
+    r.pad = (int32_t)(uint32_t)(w3 >> 32);
+    return r;
+}
+
 // a VGPR zero the compiler cannot see through: keeps uniform loads of data written by other
 // workgroups in this launch on the vector path (vmcnt, in order) instead of the scalar cache
 __device__ __forceinline__ int opaque_zero() {
@@ -377,9 +401,9 @@ __device__ __noinline__ void mw_publish(const MwTiles& T, MwShared* S, unsigned 
     }
     from = (unsigned)__builtin_amdgcn_readlane((int)from, 0);
     if (from >= upto) return;
-    // claimed [from, upto): the round's plan, bounds and tile counters were released by the
-    // committer wave before the block barrier; release again from this wave before the tasks
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // claimed [from, upto): what the tasks' scans read — the round's plan, bounds, tile counters
+    // (written through) and node rows (written through, or released) — was stored and drained by
+    // the committer wave before the block barrier this wave has passed: no fence here (R1)
     engine_publish(T.ctl, T.ring, from, upto, T.need, T.round, T.comp);
 }
 
@@ -400,7 +424,9 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the tile's outputs are read with sc1 loads (ld_through): no acquire fence; this only keeps
+    // the compiler from moving them above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     ready = tile + 1;
     return true;
 }
@@ -573,9 +599,9 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
                 MW_ACC(a_ht, tw1_ - tw0_);                                                     \
             }                                                                                  \
             _Pragma("unroll") for (int e = 0; e < MW_EPL; ++e)                                  \
-                kk[C][e] = has[e] ? cand[eoff[e] + (int64_t)tt_ * E] : KEY_INF;                \
-            jr[C] = ld_job(wjob + P.slot0 + tt_);                                              \
-            jbd[C] = bnd[P.slot0 + tt_];                                                       \
+                kk[C][e] = has[e] ? ld_through(cand + eoff[e] + (int64_t)tt_ * E) : KEY_INF;   \
+            jr[C] = ld_job_through(wjob + P.slot0 + tt_);                                      \
+            jbd[C] = ld_through(bnd + P.slot0 + tt_);                                          \
         }                                                                                      \
         /* snapshot: the decider has resolved at least i - (MW_M - 1) records (and so has read  \
            record slot i & 7's previous one) */                                                \
@@ -734,9 +760,9 @@ __device__ __noinline__ void mw_helper(const CompPlan& Pref, MwShared* Sin,
         if (!mw_tile_ready(T, tt, ready, S)) return;  // halted / watchdog
 #pragma unroll
         for (int e = 0; e < MW_EPL; ++e)
-            kk[s][e] = has[e] ? cand[eoff[e] + (int64_t)tt * E] : KEY_INF;
-        jr[s] = ld_job(wjob + P.slot0 + tt);
-        jbd[s] = bnd[P.slot0 + tt];
+            kk[s][e] = has[e] ? ld_through(cand + eoff[e] + (int64_t)tt * E) : KEY_INF;
+        jr[s] = ld_job_through(wjob + P.slot0 + tt);
+        jbd[s] = ld_through(bnd + P.slot0 + tt);
     }
 #pragma unroll
     for (int e = 0; e < MW_EPL; ++e) {
@@ -1129,13 +1155,15 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
     }
     __syncthreads();
     const CommitResult r{S->res[0], S->res[1], S->res[2], S->res[3]};
-    // write the dirty rows back for the next round's scan
+    // write the dirty rows back for the next round's scan, through (sc1: the next round's
+    // publish needs no release fence for them; {cpu, mem} as one 8-B word, then gpu)
     for (int u = threadIdx.x; u < r.dirty; u += MW_WAVES * 64) {
         const MwRow w = S->rows[u];
         NodeRec* d = rec + w.pos;
-        d->cpu = w.cpu;
-        d->mem = w.mem;
-        d->gpu = w.gpu;
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(&d->cpu),
+                           (uint64_t)(uint32_t)w.cpu | ((uint64_t)(uint32_t)w.mem << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&d->gpu, w.gpu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
     __syncthreads();

@@ -124,9 +124,8 @@ __device__ __noinline__ void tm_publish(const MwTiles& T, TmShared* S, unsigned 
     }
     from = (unsigned)__builtin_amdgcn_readlane((int)from, 0);
     if (from >= upto) return;
-    // the round's plan, bounds and tile counters were released by the committer wave before the
-    // block barrier; release again from this wave before the tasks
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // what the tasks' scans read was stored through or released by the committer wave before the
+    // block barrier this wave has passed: no fence here (fit_commit_mw.h mw_publish)
     engine_publish(T.ctl, T.ring, from, upto, T.need, T.round, T.comp);
 }
 
@@ -152,7 +151,8 @@ __device__ __forceinline__ bool tm_tile_ready(const MwTiles& T, int tt, int& rea
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // sc1 loads of the tile's outputs, no acquire fence (fit_commit_mw.h ld_through)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     ready = tile + 1;
     return true;
 }
@@ -307,9 +307,9 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         if (!tm_tile_ready(T, tt, ready, S)) return false;
 #pragma unroll
         for (int c = 0; c < TM_CPL; ++c)
-            o.kk[c] = lane + 64 * c < E ? cand[P.cand_off + (int64_t)tt * E + lane + 64 * c] : KEY_INF;
-        o.J = ld_job(wjob + P.slot0 + tt);
-        o.B = bnd[P.slot0 + tt];
+            o.kk[c] = lane + 64 * c < E ? ld_through(cand + P.cand_off + (int64_t)tt * E + lane + 64 * c) : KEY_INF;
+        o.J = ld_job_through(wjob + P.slot0 + tt);
+        o.B = ld_through(bnd + P.slot0 + tt);
         return true;
     };
     TmJob cur, nxt;
@@ -1049,17 +1049,24 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
         const int n = rfl(s.cnt);
         Seg* dst = slab + (int64_t)p * TL_MAX_SLOTS;
         Seg hd = Seg{H, -1, -1, -1};
+        // written through (two 8-B sc1 stores per run): the release at the next round's start then
+        // finds few dirty L2 lines to write back (fit_engine_ctl.h store_through)
+        auto put = [](Seg* d, const Seg& v) {
+            uint64_t* w = reinterpret_cast<uint64_t*>(d);
+            store_through64(w, (uint64_t)(uint32_t)v.end | ((uint64_t)(uint32_t)v.cpu << 32));
+            store_through64(w + 1, (uint64_t)(uint32_t)v.mem | ((uint64_t)(uint32_t)v.gpu << 32));
+        };
         if (!gl) {
             const Seg* src = lr + l * RS;
             if (lane < n) {
                 hd = src[lane];
-                dst[lane] = hd;
+                put(dst + lane, hd);
             }
         } else if (lane < TL_HEAD && lane < n) {
             hd = dst[lane];
         }
-        if (lane < TL_HEAD) hdr[p].head[lane] = hd;
-        if (lane == 0) hdr[p].cnt = n;
+        if (lane < TL_HEAD) put(&hdr[p].head[lane], hd);
+        if (lane == 0) __hip_atomic_store(&hdr[p].cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
 #ifdef FIT_STAMPS

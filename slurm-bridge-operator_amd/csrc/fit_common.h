@@ -147,6 +147,25 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
     }
 }
 
+// A window job row for the commit: written through (four 8-B agent-scope stores, sc1) when the
+// commit runs in the same launch (see scan_tile), a plain store otherwise.
+template <bool THROUGH>
+__device__ __forceinline__ void store_job(JobRec* dst, const JobRec& J) {
+    if constexpr (THROUGH) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+        const uint64_t w0 = (uint64_t)(uint32_t)J.q | ((uint64_t)(uint32_t)J.cpu << 32);
+        const uint64_t w1 = (uint64_t)(uint32_t)J.mem | ((uint64_t)(uint32_t)J.gpu << 32);
+        const uint64_t w2 = (uint64_t)(uint32_t)J.wall | ((uint64_t)J.pbit << 32);
+        const uint64_t w3 = (uint64_t)(uint32_t)J.k | ((uint64_t)(uint32_t)J.pad << 32);
+        __hip_atomic_store(d + 0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 2, w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 3, w3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *dst = J;
+    }
+}
+
 // -------------------------------------------------------------------------------- k_scan
 // Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices (one per wave).
 // Each wave keeps the exact top-K of its sub-slice; the 8 lists are merged through LDS in a
@@ -164,6 +183,21 @@ __device__ __forceinline__ void scan_row(const NodeRec& r, int x, const JobRec& 
 // LDS.  The plain path's scalar loads, four rows per wait, pay one round trip per four rows: after
 // the acquire that opens every task the rows come from MALL / HBM, and a lone first tile (nothing
 // else runs on its CU to hide the latency) spent most of its ~19 us waiting (C3).
+#ifdef FIT_TILE0_STAMPS  // diagnostic build only: where a staged first tile's time goes
+__device__ unsigned long long g_tile0[8];
+#define T0_MARK(i)                                                                              \
+    do {                                                                                        \
+        if (STAGE) {                                                                            \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                         \
+            const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                   \
+            if (threadIdx.x == 0 && (i) > 0) atomicAdd(&g_tile0[(i) - 1], now_ - t0m_);         \
+            if ((i) == 0 && threadIdx.x == 0) atomicAdd(&g_tile0[7], 1ull);                     \
+            t0m_ = now_;                                                                        \
+        }                                                                                       \
+    } while (0)
+#else
+#define T0_MARK(i)
+#endif
 template <bool PERSISTENT, int K, int KW = K, bool STAGE = false>
 __device__ __forceinline__ void scan_tile(
     const CompPlan& P, int tile, int s, const NodeRec* __restrict__ rec,
@@ -178,6 +212,10 @@ __device__ __forceinline__ void scan_tile(
     const int lane = threadIdx.x & 63;
     const int t = tile * SCAN_JOBS + lane;
     const bool active = t < P.w;
+#ifdef FIT_TILE0_STAMPS
+    unsigned long long t0m_ = 0;
+#endif
+    T0_MARK(0);
 
     JobRec J;
     J.q = active ? jl[P.jbase + t] : 0;
@@ -205,8 +243,10 @@ __device__ __forceinline__ void scan_tile(
         const v4* src = reinterpret_cast<const v4*>(rec + a);
         v4* dst = reinterpret_cast<v4*>(stage);
         const int nv = 2 * max(b - a, 0);  // two 16-B halves per 32-B row
+        T0_MARK(1);
         for (int i = threadIdx.x; i < nv; i += SCAN_WAVES * 64) dst[i] = src[i];
         __syncthreads();
+        T0_MARK(2);
         int x = n0;
         for (; x + 4 <= n1; x += 4) {
             NodeRec r[4];
@@ -216,6 +256,7 @@ __device__ __forceinline__ void scan_tile(
             for (int u = 0; u < 4; ++u) scan_row(r[u], x + u, J, key, lim);
         }
         for (; x < n1; ++x) scan_row(stage[x - a], x, J, key, lim);
+        T0_MARK(3);
     } else {
         int x = n0;
         for (; x + 4 <= n1; x += 4) {  // 4 rows per batch: four scalar row loads per wait
@@ -244,23 +285,34 @@ __device__ __forceinline__ void scan_tile(
         }
         __syncthreads();
     }
+    T0_MARK(4);
     if (feas != nullptr && wave == 0) {  // the tile's jobs with a fitting node in this block-slice
         const uint64_t fm = __ballot(active && key[0] != KEY_INF);
         if (lane == 0 && fm != 0ull) atomicOr(feas, (unsigned long long)fm);
     }
     if (wave != 0 || !active) return;  // (no barrier follows inside scan_tile)
     uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KW;
+    if constexpr (PERSISTENT) {
+        // the commit of the same launch reads these: written through (sc1 stores, agent-scope
+        // atomics) so the worker needs no release fence before it counts the tile done — the
+        // fence's write-back of the XCD's L2 cost every task a few us (MI355X_MICROARCH.md,
+        // fence table; cdna_hip_programming.md §6 Guideline 16 R1)
 #pragma unroll
-    for (int i = 0; i < KW; i += 2) {
-        ulonglong2 v;
-        v.x = i < K ? key[i] : KEY_INF;
-        v.y = i + 1 < K ? key[i + 1] : KEY_INF;
-        *reinterpret_cast<ulonglong2*>(dst + i) = v;
+        for (int i = 0; i < KW; ++i)
+            __hip_atomic_store(dst + i, i < K ? key[i] : KEY_INF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+#pragma unroll
+        for (int i = 0; i < KW; i += 2) {
+            ulonglong2 v;
+            v.x = i < K ? key[i] : KEY_INF;
+            v.y = i + 1 < K ? key[i + 1] : KEY_INF;
+            *reinterpret_cast<ulonglong2*>(dst + i) = v;
+        }
     }
     if (key[K - 1] != KEY_INF)
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
                   (unsigned long long)key[K - 1]);
-    if (s == 0) wjob[P.slot0 + t] = J;
+    if (s == 0) store_job<PERSISTENT>(wjob + P.slot0 + t, J);
 }
 
 // ------------------------------------------------------------------------------ k_commit

@@ -93,6 +93,21 @@ __device__ __forceinline__ void engine_publish(EngineCtl* ctl, unsigned long lon
     }
 }
 
+// Write-through (sc1) copy of a small record by the lanes of one wave: 8-B relaxed agent-scope
+// stores (cdna_hip_programming.md §6 Guideline 16 R1), so it needs no release fence of its own.
+template <class T>
+__device__ __forceinline__ void store_through(T* dst, const T& v) {
+    static_assert(sizeof(T) % 8 == 0, "8-byte words");
+    const unsigned lane = threadIdx.x & 63u;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(&v);
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+    for (unsigned i = lane; i < sizeof(T) / 8; i += 64)
+        __hip_atomic_store(d + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_through64(uint64_t* dst, uint64_t v) {
+    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void acquire_agent() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

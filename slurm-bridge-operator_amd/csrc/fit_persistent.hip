@@ -62,6 +62,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
+        bool prev_multi = false;  // the previous round ran the single-wave commit (plain row stores)
         while (cursor < S.jend) {
             const int w = min(win, S.jend - cursor);
             const unsigned rnd = (unsigned)rounds + 1u;  // task round tag
@@ -93,13 +94,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 // previous round's may still be in flight, in the other set
                 bool fail = !wait_tiles(ctl, c, par, target[par]);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
-                if (lane == 0) plans[2 * c + par] = P;
-                for (int i = lane; i < w; i += 64) bnd[P.slot0 + i] = KEY_INF;
+                // written through (sc1), like the tile counters: the helpers that publish tiles
+                // just in time need no release of their own (R1: stored, drained, then the
+                // block barrier, then their task stores)
+                store_through(&plans[2 * c + par], P);
+                for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64) {
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&ctl->tfeas[par][c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                release_agent();  // plan, bound / counter reset and last round's node rows → visible
+                // node rows: the multi-wave commit writes them back through (commit_window_mw);
+                // the single-wave commit of a multi-node window writes them plainly: release those
+                if (prev_multi) release_agent();
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 // just-in-time publishing (ENGINE_AHEAD > 0, k = 1 windows): the first
                 // ENGINE_AHEAD job tiles now, the rest by the helpers as they reach them
                 // (fit_commit_mw.h mw_publish), so the ring never holds a whole window of tiles
@@ -168,6 +175,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 4u);
                 break;
             }
+            prev_multi = multi;
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
             tw += t1 - t0;
             tc += t2 - t1;
@@ -286,13 +294,15 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (!skip) release_agent();
+            // the tile's outputs were written through (scan_tile: sc1 stores, agent atomics) and
+            // every storing wave waited for them (vmcnt(0) above, then the barrier): the counts
+            // need no release fence (cdna_hip_programming.md §6 Guideline 16 R1)
             __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();  // task_slot is rewritten by thread 0 next iteration
@@ -333,6 +343,11 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
 
 }  // namespace fitgpu
 
+#ifdef FIT_TILE0_STAMPS
+extern "C" int fit_debug_tile0(unsigned long long* out /* 8 */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fitgpu::g_tile0), sizeof(fitgpu::g_tile0)) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef FIT_STAMPS
 extern "C" int fit_debug_mw_stamps(unsigned long long* out /* 64 x 16 */) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(fitgpu::g_mw), sizeof(fitgpu::g_mw)) == hipSuccess

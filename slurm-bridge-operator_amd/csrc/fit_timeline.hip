@@ -372,17 +372,15 @@ __device__ __forceinline__ void scan_tile_tl(
     }
     if (wave != 0 || !active) return;
     uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * TL_KS;
+    // written through (sc1): k_engine_tl's commit reads them in the same launch and the worker
+    // counts the tile done with no release fence (scan_tile, fit_common.h)
 #pragma unroll
-    for (int i = 0; i < TL_KS; i += 2) {
-        ulonglong2 v;
-        v.x = key[i];
-        v.y = key[i + 1];
-        *reinterpret_cast<ulonglong2*>(dst + i) = v;
-    }
+    for (int i = 0; i < TL_KS; ++i)
+        __hip_atomic_store(dst + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (key[TL_KS - 1] != KEY_INF)
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
                   (unsigned long long)key[TL_KS - 1]);
-    if (s == 0) wjob[P.slot0 + t] = J;
+    if (s == 0) store_job<true>(wjob + P.slot0 + t, J);
 }
 
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
@@ -1020,8 +1018,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 // its stop) must all be complete before their buffers and counters are reused
                 bool f = !wait_tiles(ctl, c, par, target[par]);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
-                if (lane == 0) plans[2 * c + par] = P;
-                for (int i = lane; i < w; i += 64) bnd[P.slot0 + i] = KEY_INF;
+                store_through(&plans[2 * c + par], P);  // as k_engine's (fit_persistent.hip)
+                for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 release_agent();  // plan, bound / counter reset and the last window's run lists
@@ -1163,13 +1161,14 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (!skip) release_agent();
+            // the tile's outputs were written through and every storing wave waited for them
+            // (vmcnt(0) above, then the barrier): the counts need no release fence (R1)
             __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->done[c][2 + par], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             busy += (int64_t)__builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();  // task_slot is rewritten by thread 0 next iteration
