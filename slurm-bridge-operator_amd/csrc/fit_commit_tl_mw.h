@@ -31,11 +31,6 @@
 namespace fitgpu {
 
 constexpr int TM_M = 8;   // items per record (> snapshot lag)
-#ifndef TM_PREP
-#define TM_PREP 0  // 1: the helper reserves this job's window on its staged (first clean) item's list
-                   // itself, prefix minima included; a decider whose winner is that item copies the
-                   // prepared list into the new dirty slot instead of running tm_reserve
-#endif
 constexpr int TM_R = 8;   // record ring
 constexpr int TM_H = SCAN_WAVES - 1;  // helpers: waves 1..7
 static_assert(TM_H >= 1 && TM_H <= SCAN_WAVES - 1, "helpers are waves 1..7");
@@ -81,9 +76,6 @@ struct alignas(16) TmShared {
     uint32_t pad[7];
     TmRec rec[TM_R];
     Seg stage[TM_R][64];     // the run list of each record's first clean item
-#if TM_PREP
-    int4 stagepm[TM_R][64];  // TM_PREP: its prefix minima (the stage then holds the reserved list)
-#endif
     TmSlot slot[TL_UCAP];
     Seg scr[TL_MAX_SLOTS];   // general-path scratch (tl_reserve_any)
     // followed by: run-list regions (TL_UCAP x RS Seg), their prefix minima (TL_UCAP x RS int4),
@@ -474,30 +466,17 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         if (ix1)
             Rr->it[ix1 - 1u] = TmItem{(uint32_t)xd, (uint32_t)(xd >> 32), lane, si.orig, si.mask, si.cnt,
                                       si.cc, si.cm, si.cg, 0, 0, 0};
-        int32_t scnt = 0, pcnt = -1;  // pcnt: run count of the prepared (reserved) list, -1: none
+        int32_t scnt = 0;
         if (spos != 0xffffffffu) {
             scnt = readlane(fc == 0 ? ch[0].cnt : ch[TM_CPL - 1].cnt, fl);
-#if TM_PREP
-            if (scnt <= R) {
-                // the item's start is in its key; a surviving item's node is unchanged since this
-                // snapshot, so the list after this job's reservation is what the decider would
-                // compute.  Run 63 of the stage is never a real output (lists hold <= R < 64
-                // runs): tm_reserve's lanes without a write go there.
-                const int32_t s0 = readlane((int32_t)((fc == 0 ? xc[0] : xc[TM_CPL - 1]) >> 54), fl);
-                Seg* const st = &S->stage[t & (TM_R - 1)][0];
-                pcnt = tm_reserve(lds_addr(st), lds_addr(&S->stagepm[t & (TM_R - 1)][0]),
-                                  lds_addr(st + 63), srun, scnt, R, s0, s0 + jd, jc, jm, jg);
-            }
-#else
             if (scnt <= R && lane < scnt) S->stage[t & (TM_R - 1)][lane] = srun;
-#endif
         }
         const uint32_t spos2w = 0xffffffffu;  // header words of a second staged list (none)
         const int32_t scnt2 = 0;
         if (lane == 0) {
             *reinterpret_cast<v4i32*>(&Rr->h.jc) = v4i32{jc, jm, jg, jd};
             *reinterpret_cast<v4u32*>(&Rr->h.pbit) = v4u32{jp, spos, (uint32_t)scnt, spos2w};
-            *reinterpret_cast<v4u32*>(&Rr->h.blo) = v4u32{(uint32_t)B, (uint32_t)(B >> 32), (uint32_t)scnt2, (uint32_t)pcnt};
+            *reinterpret_cast<v4u32*>(&Rr->h.blo) = v4u32{(uint32_t)B, (uint32_t)(B >> 32), (uint32_t)scnt2, 0xffffffffu};
             Rr->h.v = v;
             Rr->h.n = n;
             Rr->h.q = J.q;
@@ -785,28 +764,14 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         // slab), an LDS list's from its region; tm_reserve writes the whole new list
         Seg g{0, 0, 0, 0};
         int nn = -1;
-#if TM_PREP
-        bool prepped = false;  // the helper already reserved this job on the staged list
-#endif
         if (fresh) {  // a clean winner becomes dirty slot nu
             glob = cnt > X.R;
             if (!glob) {
                 // typed loads on both sides: a plain select of the two pointers becomes one flat
                 // load, which waits on the vector-memory path even for the LDS stage
                 if (cur.h2.y == pos && (int32_t)cur.h2.z == cnt) {  // staged by the helper
-#if TM_PREP
-                    // reserved at the item's start, which is the winner's start (a surviving item's
-                    // key is current); not prepared (it would outgrow R): the node's list is the
-                    // slab's, unchanged since the snapshot
-                    prepped = (int32_t)cur.h3.w >= 0;
-                    if (!prepped) {
-                        const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
-                        g = Seg{x.x, x.y, x.z, x.w};
-                    }
-#else
                     const v4u32 x = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
                     g = Seg{(int32_t)x.x, (int32_t)x.y, (int32_t)x.z, (int32_t)x.w};
-#endif
                 } else {  // not the staged item (written meanwhile)
                     const v4i32 x = *(const GAS v4i32*)(X.slab + (int64_t)pos * TL_MAX_SLOTS + lane);
                     g = Seg{x.x, x.y, x.z, x.w};
@@ -829,17 +794,6 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
 #ifdef FIT_STAMPS_FINE
         a1 = __builtin_amdgcn_s_memtime();
         TM_ADD(3, a1 - a0);
-#endif
-#if TM_PREP
-        if (prepped) {  // copy the helper's reserved list and prefix minima into the slot's region
-            nn = (int32_t)cur.h3.w;
-            const v4u32 a = lds4(&S->stage[t & (TM_R - 1)][lane])[0];
-            const v4u32 b = lds4(&S->stagepm[t & (TM_R - 1)][lane])[0];
-            if (lane < nn) {
-                *(lds_v4i32*)(uintptr_t)lds_addr(L + lane) = v4i32{(int32_t)a.x, (int32_t)a.y, (int32_t)a.z, (int32_t)a.w};
-                *(lds_v4i32*)(uintptr_t)lds_addr(PM + lane) = v4i32{(int32_t)b.x, (int32_t)b.y, (int32_t)b.z, (int32_t)b.w};
-            }
-        } else
 #endif
         if (!glob) {
             nn = tm_reserve(lds_addr(L), lds_addr(PM), lds_addr(&S->scr[lane]), g, cnt, X.R, start,
@@ -994,12 +948,14 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
 }
 
 // All 8 waves of the committer block call this; returns the same result in every wave.  smem:
-// engine_tl_lds_bytes(); R: LDS run-list capacity per dirty slot (engine_tl_runs).
+// engine_tl_lds_bytes(); R: LDS run-list capacity per dirty slot (engine_tl_runs).  glob: set when
+// a dirty list of the window lives in the global slab — written with plain stores, which the next
+// round must release before its scan reads them; every other write-back is stored through.
 __device__ __forceinline__ CommitResult commit_tl_window_mw(
     const CompPlan& P, unsigned char* smem, Seg* __restrict__ slab, TlHdr* __restrict__ hdr,
     const uint64_t* __restrict__ cand, const uint64_t* __restrict__ bnd,
     const JobRec* __restrict__ wjob, int32_t* __restrict__ out, int32_t* __restrict__ outs,
-    int32_t H, int32_t R, MwTiles T) {
+    int32_t H, int32_t R, MwTiles T, bool& glob) {
     TmShared* S = reinterpret_cast<TmShared*>(smem);
     const int32_t RS = R + TL_PAD;
     Seg* lr = reinterpret_cast<Seg*>(smem + sizeof(TmShared));
@@ -1041,9 +997,11 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
 #ifdef FIT_STAMPS
     const unsigned long long e0 = __builtin_amdgcn_s_memtime();
 #endif
+    glob = false;
     for (int l = 0; l < r.dirty; ++l) {
         const TmSlot s = S->slot[l];
         const bool gl = rfl(s.glob) != 0;
+        glob |= gl;
         if (gl ? wave != 0 : (l & (SCAN_WAVES - 1)) != wave) continue;
         const uint32_t p = (uint32_t)rfl((int32_t)s.pos);
         const int n = rfl(s.cnt);

@@ -994,6 +994,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity (fit_engine_ctl.h)
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         bool fail = false;
+        bool glob = false;  // the last window wrote a global-slab list (plain stores)
         while (cursor < S.jend) {
             const int w = min(win, S.jend - cursor);
             const unsigned rnd = (unsigned)rounds + 1u;  // task round tag
@@ -1022,7 +1023,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                release_agent();  // plan, bound / counter reset and the last window's run lists
+                // plan, bound / counter reset and the last window's run lists and headers were
+                // stored through (sc1; R1: drained before the publish); a global-slab list was
+                // not: release it (≈1.7-6.5 us on the round-start path otherwise)
+                if (glob) release_agent();
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 // the first TL_AHEAD job tiles now, the rest by the helpers just in time
                 // (tm_tile_ready)
                 const unsigned npub = TL_AHEAD > 0 ? min(ntj, (unsigned)TL_AHEAD) : ntj;
@@ -1049,7 +1054,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
                                     MwTiles{&ctl->tdone[par][c][0], (unsigned)S.nslice,
                                             TL_AHEAD > 0 ? ring : nullptr, ctl, rnd, (unsigned)c, ntj,
-                                            nullptr});
+                                            nullptr},
+                                    glob);
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
             // commit's closing barrier)
