@@ -443,11 +443,14 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // two sets of per-round buffers (plans, candidates, bounds, job rows) by round parity
     // (fit_engine_ctl.h): a round starts while the previous round's last tiles are still scanned
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
-        c->plan.ensure(2 * nc) || c->cand.ensure((size_t)2 * nc * per_comp_cand) ||
+        c->plan.ensure(2 * nc) ||
+        c->cand.ensure((size_t)2 * nc * per_comp_cand + (size_t)2 * nc * PAIR_AREA) ||
         c->bnd.ensure((size_t)2 * nc * wcap) || c->wjob.ensure((size_t)2 * nc * wcap) ||
         c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
         c->h_err.ensure(4))
         return FIT_E_OOM;
+    if ((int64_t)2 * nc * per_comp_cand + (int64_t)2 * nc * PAIR_AREA > INT32_MAX)
+        return fail(FIT_E_INVAL, "candidate buffer exceeds 2^31 entries (%d components)", nc);
     for (int i = 0; i < nc; ++i) {
         const int k = comps[i];
         CompState& s = c->h_ecs.p[i];
@@ -466,7 +469,7 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
         s.slot0 = (int32_t)(i * wcap);
         s.cand_alt = (int64_t)(nc + i) * per_comp_cand;
         s.slot_alt = (int32_t)((nc + i) * wcap);
-        s.pad = 0;
+        s.pair_off = (int32_t)(2 * nc * per_comp_cand + (int64_t)2 * i * PAIR_AREA);
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
@@ -475,7 +478,8 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // all (a granule overwritten before its worker read it would be lost)
     int32_t max_slices = 1;
     for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
-    if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices > (int64_t)engine_ring_tasks())
+    // (+ one tile: a round's first tile may be scanned as twice the slices, K_T0PAIR)
+    if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices > (int64_t)engine_ring_tasks())
         return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                     nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     size_t lds = engine_lds_bytes(maxnodes);
@@ -752,11 +756,14 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     const int64_t per_comp_cand = wcap * slices * TL_KS;
     // two sets of per-round buffers by round parity (see run_persistent)
     if (c->ecs.ensure(nc) || c->eco.ensure(nc) || c->h_ecs.ensure(nc) || c->h_eco.ensure(nc) ||
-        c->plan.ensure(2 * nc) || c->cand.ensure((size_t)2 * nc * per_comp_cand) ||
+        c->plan.ensure(2 * nc) ||
+        c->cand.ensure((size_t)2 * nc * per_comp_cand + (size_t)2 * nc * PAIR_AREA) ||
         c->bnd.ensure((size_t)2 * nc * wcap) || c->wjob.ensure((size_t)2 * nc * wcap) ||
         c->ectl.ensure(engine_ctl_bytes()) || c->ering.ensure(engine_ring_bytes()) ||
         c->h_err.ensure(4))
         return FIT_E_OOM;
+    if ((int64_t)2 * nc * per_comp_cand + (int64_t)2 * nc * PAIR_AREA > INT32_MAX)
+        return fail(FIT_E_INVAL, "candidate buffer exceeds 2^31 entries (%d components)", nc);
     for (int i = 0; i < nc; ++i) {
         const int k = comps[i];
         CompState& s = c->h_ecs.p[i];
@@ -772,14 +779,15 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         s.slot0 = (int32_t)(i * wcap);
         s.cand_alt = (int64_t)(nc + i) * per_comp_cand;
         s.slot_alt = (int32_t)((nc + i) * wcap);
-        s.pad = 0;
+        s.pair_off = (int32_t)(2 * nc * per_comp_cand + (int64_t)2 * i * PAIR_AREA);
         s.wmin = std::min(c->wmin, (int)wcap);
         s.wmax = (int32_t)wcap;
     }
     {  // task ring capacity (see run_persistent)
         int32_t max_slices = 1;
         for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
-        if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS) * max_slices >
+        // (+ one tile: a round's first tile may be scanned as twice the slices, TL_T0PAIR)
+        if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices >
             (int64_t)engine_ring_tasks())
             return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                         nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);

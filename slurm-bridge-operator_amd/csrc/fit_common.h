@@ -198,16 +198,22 @@ __device__ unsigned long long g_tile0[8];
 #else
 #define T0_MARK(i)
 #endif
-template <bool PERSISTENT, int K, int KW = K, bool STAGE = false>
-__device__ __forceinline__ void scan_tile(
+// PAIR (k_engine's round-first tile, K_T0PAIR; P here has half-size sub-slices over twice the
+// block-slices): as scan_tile_tl's (fit_timeline.hip) — half-slices 2p and 2p+1 each keep their
+// top K, the second to finish merges the first's list (stored through, counted in pairs[p]) into
+// slot p and sets the bound.  Returns whether the task completes its tile's block-slice (wave 0).
+template <bool PERSISTENT, int K, int KW = K, bool STAGE = false, bool PAIR = false>
+__device__ __forceinline__ bool scan_tile(
     const CompPlan& P, int tile, int s, const NodeRec* __restrict__ rec,
     const int32_t* __restrict__ jl, const int32_t* __restrict__ jcpu,
     const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
     const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
     const uint16_t* __restrict__ jk, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
     JobRec* __restrict__ wjob, uint64_t (*xk)[K][64],
-    unsigned long long* __restrict__ feas = nullptr, NodeRec* __restrict__ stage = nullptr) {
-    if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
+    unsigned long long* __restrict__ feas = nullptr, NodeRec* __restrict__ stage = nullptr,
+    unsigned* __restrict__ pairs = nullptr) {
+    static_assert(!PAIR || (PERSISTENT && K <= 4), "pair scratch: 4 keys per (job, pair)");
+    if (tile * SCAN_JOBS >= P.w) return true;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int t = tile * SCAN_JOBS + lane;
@@ -290,7 +296,45 @@ __device__ __forceinline__ void scan_tile(
         const uint64_t fm = __ballot(active && key[0] != KEY_INF);
         if (lane == 0 && fm != 0ull) atomicOr(feas, (unsigned long long)fm);
     }
-    if (wave != 0 || !active) return;  // (no barrier follows inside scan_tile)
+    if (wave != 0) return true;  // (no barrier follows inside scan_tile)
+    if constexpr (PAIR) {
+        const int ns = P.nslice >> 1, pr = s >> 1;
+        uint64_t* const fin = cand + P.cand_off + ((int64_t)t * ns + pr) * KW;
+        uint64_t* const tmp = cand + P.pair_off + ((int64_t)lane * 32 + pr) * 4;  // tile 0: t = lane
+        if (active) {
+            if (s & 1) {
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    __hip_atomic_store(tmp + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+#pragma unroll
+                for (int i = 0; i < KW; ++i)
+                    __hip_atomic_store(fin + i, i < K ? key[i] : KEY_INF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (s == 0) store_job<true>(wjob + P.slot0 + t, J);
+        }
+        // R1: the list (and the live-job bits above) stored and drained before the pair count
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = 0u;
+        if (lane == 0) prev = __hip_atomic_fetch_add(pairs + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane((int)prev) == 0) return false;  // the partner merges
+        if (active) {
+            const uint64_t* const other = (s & 1) ? fin : tmp;
+            uint64_t o[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                o[i] = __hip_atomic_load(const_cast<uint64_t*>(other + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            merge_lists(key, o);
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                __hip_atomic_store(fin + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (key[K - 1] != KEY_INF)
+                atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
+                          (unsigned long long)key[K - 1]);
+        }
+        return true;
+    }
+    if (!active) return true;
     uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * KW;
     if constexpr (PERSISTENT) {
         // the commit of the same launch reads these: written through (sc1 stores, agent-scope
@@ -313,6 +357,7 @@ __device__ __forceinline__ void scan_tile(
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
                   (unsigned long long)key[K - 1]);
     if (s == 0) store_job<PERSISTENT>(wjob + P.slot0 + t, J);
+    return true;
 }
 
 // ------------------------------------------------------------------------------ k_commit

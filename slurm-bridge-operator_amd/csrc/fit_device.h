@@ -65,7 +65,9 @@ struct alignas(16) CompPlan {
     int32_t ks;          // keys kept per (job, block-slice): KS, or fewer for a large component
     int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
     int32_t slot0;       // first window slot (global over components)
-    int32_t k0;          // persistent engine: the round's first job tile may keep FIT_K0 keys (k = 1 window)
+    int32_t k0;          // persistent engines, the round's first job tile: bit 0 keeps FIT_K0 keys
+                         // (k_engine, k = 1 window); bit 1 scans it as paired half-slices (*_T0PAIR)
+    int32_t pair_off;    // u64 offset of the round's half-slice list scratch (bit 1 of k0)
 };
 
 // Persistent engine (fit_persistent.hip): per-component state written by the host, results
@@ -79,7 +81,7 @@ struct CompState {
     int32_t ks;            // keys per (job, block-slice) (CompPlan::ks)
     int64_t cand_alt;      // the same for odd rounds (fit_engine_ctl.h: two buffer sets by parity)
     int32_t slot_alt;
-    int32_t pad;
+    int32_t pair_off;      // half-slice list scratch (even rounds; odd: + PAIR_AREA)
 };
 
 struct CompOut {
@@ -102,6 +104,10 @@ constexpr int TL_UCAP = TL_UCAP_DEF;  // dirty nodes per component per round (TL
 constexpr int TL_CAND = FIT_TL_CAND;  // candidates per job of the timeline scan (64 or 128)
 static_assert((TL_CAND == 64 || TL_CAND == 128) && TL_CAND % TL_KS == 0, "FIT_TL_CAND: 64 or 128");
 constexpr int TL_SLICES = TL_CAND / TL_KS;  // block-slices per job (over all ranks) in the timeline scan
+// The persistent engines' paired first tile (K_T0PAIR, TL_T0PAIR): one half-slice list of up to 4
+// keys per (job, pair) held until its partner half merges it, per component and round parity
+constexpr int PAIR_AREA = SCAN_JOBS * 32 * 4;
+static_assert(TL_KS <= 4, "pair scratch holds 4 keys per (job, pair)");
 constexpr int TL_MIN_SUB = 16;      // minimum nodes per wave sub-slice in the timeline scan (C5: 32 block-slices;
                                     // 32 gave 25 slices, 100 candidates: 129.8 vs 127.1 ms, r03j)
 constexpr int TL_POS_BITS = 22;     // key = start << 54 | score << 22 | position

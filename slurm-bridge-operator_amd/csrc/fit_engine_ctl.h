@@ -7,7 +7,7 @@
 namespace fitgpu {
 
 #ifndef FIT_QCAP_LOG2
-#define FIT_QCAP_LOG2 17
+#define FIT_QCAP_LOG2 18
 #endif
 constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
@@ -35,6 +35,9 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     // unplaced whatever the round decides before it (node state only shrinks within a
     // placement): the commit skips it (fit_commit_mw.h, "live jobs")
     unsigned long long tfeas[2][32][ENGINE_TILES];
+    // k_engine_tl's round-first tile scanned as pairs of half-slices (TL_T0PAIR): per parity,
+    // component and pair, the halves finished (the second merges both lists)
+    unsigned tpair[2][32][32];
     unsigned long long pub[32];        // FIT_STAMPS: realtime of each component's last publish
 };
 

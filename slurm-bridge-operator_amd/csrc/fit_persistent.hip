@@ -32,6 +32,12 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
     return commit_window<MW_EPL>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
 }
 
+#ifndef FIT_K0
+#define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
+#endif
+#ifndef K_T0PAIR
+#define K_T0PAIR 1  // k_engine: a k = 1 window's first job tile as 2 x nslice half-size block-slices, paired
+#endif
 // A round's first job tile stages its block-slice's node rows in LDS behind the merge buffer and
 // the task slot (scan_tile STAGE) when they fit: SCAN_WAVES * P.sub <= STAGE_ROWS (C3: 8 x 98).
 constexpr size_t STAGE_OFF = (sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64 + 16 + 63) & ~(size_t)63;
@@ -85,7 +91,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // handles k > 1) after its whole scan; the decider/helper pipeline covers k = 1
             // windows and starts at once: helpers wait per job tile (MwTiles)
             const bool multi = jpk[cursor + w] != jpk[cursor];
-            P.k0 = multi ? 0 : 1;  // a multi-node job needs k <= KS keys in its first tile
+            // a multi-node job needs k <= KS keys in its first tile; a k = 1 window's first tile
+            // keeps FIT_K0 keys per block-slice and is scanned as paired half-slices (K_T0PAIR)
+            const bool pair = !multi && K_T0PAIR && 2 * S.nslice <= 64 && FIT_K0 > 0 && FIT_K0 < S.ks;
+            P.k0 = multi ? 0 : (1 | (pair ? 2 : 0));
+            P.pair_off = S.pair_off + (par ? PAIR_AREA : 0);
             MW_CLK(rs0);
             if (wave == 0) {
                 t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -103,6 +113,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&ctl->tfeas[par][c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+                if (pair && lane < 32)
+                    __hip_atomic_store(&ctl->tpair[par][c][lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // node rows: the multi-wave commit writes them back through (commit_window_mw);
                 // the single-wave commit of a multi-node window writes them plainly: release those
                 if (prev_multi) release_agent();
@@ -123,7 +135,13 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 }
 #endif
-                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                if (pair) {  // tile 0 as 2 x nslice half-slices, then the rest
+                    engine_publish(ctl, ring, 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
+                    if (npub > 1u) engine_publish(ctl, ring, 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                    target[par] += (unsigned)S.nslice;  // tile 0's extra tasks
+                } else {
+                    engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                }
                 if (npub == ntj) target[par] += ntiles;  // else: after the commit (M->pubt)
                 if (multi && !fail) fail = !wait_tiles(ctl, c, par, target[par]);
                 if (fail && lane == 0) atomicOr(&ctl->error, 1u);
@@ -244,21 +262,33 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         const int s = (int)task_slice(task);
         const int tile = (int)task_tile(task);
         const int par = (int)(task_round(task) & 1u);  // the round's buffer set
+        bool counts = true;  // (thread 0) the task completes its tile's block-slice (K_T0PAIR)
         if (!skip) {
             if (threadIdx.x == 0) acquire_agent();
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
-            const CompPlan P = plans[2 * c + par];
-#ifndef FIT_K0
-#define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
-#endif
+            CompPlan P = plans[2 * c + par];
+            const bool pair = tile == 0 && (P.k0 & 2);  // half-size block-slices, paired
+            if (pair) {
+                P.sub = (P.sub + 1) / 2;
+                P.nslice *= 2;
+            }
             switch (P.ks) {  // block-uniform; the host picks one of these (engine.cpp)
 #define SCAN_K(K_)                                                                               \
     case K_:                                                                                      \
         if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0) {                                     \
             constexpr int K0_ = (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_);                        \
             uint64_t(*xk0)[K0_][64] = reinterpret_cast<uint64_t(*)[K0_][64]>(smem);               \
-            if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                              \
+            if (pair && SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                      \
+                counts = scan_tile<true, K0_, K_, true, true>(                                    \
+                    P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0,   \
+                    &ctl->tfeas[par][c][tile], reinterpret_cast<NodeRec*>(smem + STAGE_OFF),         \
+                    &ctl->tpair[par][c][0]);                                                      \
+            else if (pair)                                                                        \
+                counts = scan_tile<true, K0_, K_, false, true>(                                   \
+                    P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0,   \
+                    &ctl->tfeas[par][c][tile], nullptr, &ctl->tpair[par][c][0]);                  \
+            else if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                         \
                 scan_tile<true, K0_, K_, true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, \
                                                jk, cand, bnd, wjob, xk0, &ctl->tfeas[par][c][tile],    \
                                                reinterpret_cast<NodeRec*>(smem + STAGE_OFF));     \
@@ -297,7 +327,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // the tile's outputs were written through (scan_tile: sc1 stores, agent atomics) and
             // every storing wave waited for them (vmcnt(0) above, then the barrier): the counts
             // need no release fence (cdna_hip_programming.md §6 Guideline 16 R1)
-            __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (counts)
+                __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned

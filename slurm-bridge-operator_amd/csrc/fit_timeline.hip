@@ -222,12 +222,12 @@ __global__ void k_build_tl(const int32_t* __restrict__ cpu, const int32_t* __res
 // block-slice and the runs TL_HEAD .. TL_HEAD + TL_STAGE_RUNS - 1 of every node in LDS: `r8` (that
 // node's staged runs) replaces the slab for them.
 constexpr int TL_STAGE_RUNS = 8;
-template <bool STAGE = false>
+template <bool STAGE = false, int K = TL_KS>
 __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec& J, int32_t H,
-                                             const Seg* __restrict__ slab, uint64_t (&key)[TL_KS],
+                                             const Seg* __restrict__ slab, uint64_t (&key)[K],
                                              unsigned long long& batches,
                                              const Seg* __restrict__ r8 = nullptr) {
-    const uint64_t cut = key[TL_KS - 1];
+    const uint64_t cut = key[K - 1];
     const int32_t lim = cut == KEY_INF ? H : (int32_t)(cut >> 54);
     TlWalk w = tl_walk0((h.mask & J.pbit) != 0u && J.wall <= H && J.cpu <= h.cpu &&
                         J.mem <= h.mem && J.gpu <= h.gpu);
@@ -258,11 +258,18 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
         }
     }
     const uint64_t wk = tl_walk_key(w, J.cpu, J.mem, J.gpu, (uint32_t)x);
-    if (wk < key[TL_KS - 1]) topk_insert(key, wk);
+    if (wk < key[K - 1]) topk_insert(key, wk);
 }
 
 // One scan tile: SCAN_JOBS window jobs × block-slice s of the component (host-driven k_scan_tl
 // and the persistent k_engine_tl workers).  xk: LDS merge buffer.
+// PAIR (k_engine_tl's round-first tile, TL_T0PAIR; P here has half-size sub-slices over twice the
+// block-slices): half-slices 2p and 2p+1 each keep their top TL_KS; the half that finishes first
+// stores its list (the even half in the candidate slot of block-slice p, the odd half in the
+// plan's pair scratch) and counts itself in `pairs[p]`, the second merges the other's list with
+// its own into slot p and sets the bound — the same (list, bound) per block-slice as one
+// full-size task, from two tasks on two CUs (the commit waits for this tile at every round
+// start).  Returns whether the task completes its job tile's block-slice (wave 0).
 // STAGE (k_engine_tl's first job tile of a round, which the commit waits for; needs
 // SCAN_WAVES * P.sub <= TL_STAGE_NODES): the block first copies its block-slice's headers and every
 // node's runs TL_HEAD .. TL_HEAD + TL_STAGE_RUNS - 1 into LDS with vector loads from all 512 lanes
@@ -270,16 +277,16 @@ __device__ __forceinline__ void tl_scan_node(const TlHdr& h, int x, const JobRec
 // another round trip (a lone first tile has nothing on its CU to hide them: ~40 us per task, C5).
 constexpr int TL_STAGE_NODES = 256;
 constexpr size_t TL_STAGE_BYTES = (sizeof(TlHdr) + sizeof(Seg) * TL_STAGE_RUNS) * TL_STAGE_NODES;
-template <bool STAGE = false>
-__device__ __forceinline__ void scan_tile_tl(
+template <bool STAGE = false, int K = TL_KS, bool PAIR = false>
+__device__ __forceinline__ bool scan_tile_tl(
     const CompPlan& P, int tile, int s, const Seg* __restrict__ slab,
     const TlHdr* __restrict__ hdr, const int32_t* __restrict__ jl,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
-    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[TL_KS][64],
-    unsigned char* __restrict__ stage = nullptr) {
-    if (tile * SCAN_JOBS >= P.w) return;  // block-uniform
+    JobRec* __restrict__ wjob, int32_t H, int32_t slot_min, uint64_t (*xk)[K][64],
+    unsigned char* __restrict__ stage = nullptr, unsigned* __restrict__ pairs = nullptr) {
+    if (tile * SCAN_JOBS >= P.w) return true;  // block-uniform
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int t = tile * SCAN_JOBS + lane;
@@ -297,9 +304,9 @@ __device__ __forceinline__ void scan_tile_tl(
     J.k = 1;
     J.pad = 0;
 
-    uint64_t key[TL_KS];
+    uint64_t key[K];
 #pragma unroll
-    for (int i = 0; i < TL_KS; ++i) key[i] = KEY_INF;
+    for (int i = 0; i < K; ++i) key[i] = KEY_INF;
     const int n0 = P.sb + (s * SCAN_WAVES + wave) * P.sub;
     const int n1 = min(P.se, n0 + P.sub);
     unsigned long long batches = 0, longn = 0;
@@ -327,18 +334,18 @@ __device__ __forceinline__ void scan_tile_tl(
         for (int x = n0; x < n1; ++x) {
             const TlHdr h = sh[x - a];
             longn += h.cnt > TL_HEAD;
-            tl_scan_node<true>(h, x, J, H, slab, key, batches, sr + (x - a) * TL_STAGE_RUNS);
+            tl_scan_node<true, K>(h, x, J, H, slab, key, batches, sr + (x - a) * TL_STAGE_RUNS);
         }
     } else if (n0 < n1) {
         const int z = tl_vzero();
         TlHdr h0 = hdr[n0 + z], h1 = hdr[min(n0 + 1, n1 - 1) + z];
         for (int x = n0; x < n1; x += 2) {
             longn += h0.cnt > TL_HEAD;
-            tl_scan_node(h0, x, J, H, slab, key, batches);
+            tl_scan_node<false, K>(h0, x, J, H, slab, key, batches);
             h0 = hdr[min(x + 2, n1 - 1) + z];
             if (x + 1 < n1) {
                 longn += h1.cnt > TL_HEAD;
-                tl_scan_node(h1, x + 1, J, H, slab, key, batches);
+                tl_scan_node<false, K>(h1, x + 1, J, H, slab, key, batches);
                 h1 = hdr[min(x + 3, n1 - 1) + z];
             }
         }
@@ -359,28 +366,62 @@ __device__ __forceinline__ void scan_tile_tl(
     for (int h = SCAN_WAVES / 2; h >= 1; h >>= 1) {
         if (wave >= h && wave < 2 * h) {
 #pragma unroll
-            for (int i = 0; i < TL_KS; ++i) xk[wave - h][i][lane] = key[i];
+            for (int i = 0; i < K; ++i) xk[wave - h][i][lane] = key[i];
         }
         __syncthreads();
         if (wave < h) {
-            uint64_t o[TL_KS];
+            uint64_t o[K];
 #pragma unroll
-            for (int i = 0; i < TL_KS; ++i) o[i] = xk[wave][i][lane];
+            for (int i = 0; i < K; ++i) o[i] = xk[wave][i][lane];
             merge_lists(key, o);
         }
         __syncthreads();
     }
-    if (wave != 0 || !active) return;
-    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * TL_KS;
+    if (wave != 0) return true;
+    if constexpr (PAIR) {
+        const int ns = P.nslice >> 1, pr = s >> 1;
+        uint64_t* const fin = cand + P.cand_off + ((int64_t)t * ns + pr) * K;
+        uint64_t* const tmp = cand + P.pair_off + ((int64_t)lane * 32 + pr) * K;  // tile 0: t = lane
+        uint64_t* const mine = (s & 1) ? tmp : fin;
+        uint64_t* const other = (s & 1) ? fin : tmp;
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                __hip_atomic_store(mine + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s == 0) store_job<true>(wjob + P.slot0 + t, J);
+        }
+        // R1: the list stored through and drained before the count the partner reads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = 0u;
+        if (lane == 0) prev = __hip_atomic_fetch_add(pairs + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane((int)prev) == 0) return false;  // the partner merges
+        if (active) {
+            uint64_t o[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                o[i] = __hip_atomic_load(other + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            merge_lists(key, o);
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                __hip_atomic_store(fin + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (key[K - 1] != KEY_INF)
+                atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
+                          (unsigned long long)key[K - 1]);
+        }
+        return true;
+    }
+    if (!active) return true;
+    uint64_t* dst = cand + P.cand_off + ((int64_t)t * P.nslice + s) * K;
     // written through (sc1): k_engine_tl's commit reads them in the same launch and the worker
     // counts the tile done with no release fence (scan_tile, fit_common.h)
 #pragma unroll
-    for (int i = 0; i < TL_KS; ++i)
+    for (int i = 0; i < K; ++i)
         __hip_atomic_store(dst + i, key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (key[TL_KS - 1] != KEY_INF)
+    if (key[K - 1] != KEY_INF)
         atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
-                  (unsigned long long)key[TL_KS - 1]);
+                  (unsigned long long)key[K - 1]);
     if (s == 0) store_job<true>(wjob + P.slot0 + t, J);
+    return true;
 }
 
 __global__ __launch_bounds__(SCAN_WAVES * 64) void k_scan_tl(
@@ -963,6 +1004,9 @@ namespace fitgpu {
 // per CU when the committer's 160 KB of LDS and its helpers' VGPRs size every block of the launch).
 // A MODE 1 block counts itself into `resident` (host-mapped) so that the host launches the
 // workers only once every committer holds its CU.
+#ifndef TL_T0PAIR
+#define TL_T0PAIR 1  // k_engine_tl: a round's first job tile as 2 x nslice half-size block-slices, paired
+#endif
 // the worker's LDS: merge buffer, task slot, then the first tile's stage (scan_tile_tl STAGE)
 constexpr size_t TL_STAGE_OFF = (sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64 + 16 + 63) & ~(size_t)63;
 
@@ -1012,7 +1056,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             P.blk0 = 0;
             P.cand_off = par ? S.cand_alt : S.cand_off;
             P.slot0 = par ? S.slot_alt : S.slot0;
-            P.k0 = 0;
+            // the round's first job tile as pairs of half-slices (scan_tile_tl PAIR): the commit
+            // waits for it at every round start
+            P.k0 = (TL_T0PAIR && 2 * S.nslice <= 64) ? 2 : 0;
+            P.pair_off = S.pair_off + (par ? PAIR_AREA : 0);
             const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
             if (wave == 0) {
                 // the tiles of the window before last (this round's buffer set; also those past
@@ -1023,6 +1070,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane < 32) __hip_atomic_store(&ctl->tpair[par][c][lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // plan, bound / counter reset and the last window's run lists and headers were
                 // stored through (sc1; R1: drained before the publish); a global-slab list was
                 // not: release it (≈1.7-6.5 us on the round-start path otherwise)
@@ -1038,7 +1086,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 }
 #endif
-                engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                if (P.k0 & 2) {
+                    engine_publish(ctl, ring, 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
+                    if (npub > 1u) engine_publish(ctl, ring, 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                } else {
+                    engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                }
                 if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
                 if (f && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // run lists written back by this block: CU-wide fresh view
@@ -1059,7 +1112,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
             // commit's closing barrier)
-            if (wave == 0) target[par] += reinterpret_cast<TmShared*>(smem)->pubt * (unsigned)S.nslice;
+            if (wave == 0)
+                target[par] += (reinterpret_cast<TmShared*>(smem)->pubt + ((P.k0 & 2) ? 1u : 0u)) * (unsigned)S.nslice;
             if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
             if (r.stop == 3) {
                 fail = true;
@@ -1142,12 +1196,25 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const int s = (int)task_slice(task);
         const int tile = (int)task_tile(task);
         const int par = (int)(task_round(task) & 1u);  // the round's buffer set
+        bool counts = true;  // (thread 0) the task completes its tile's block-slice (TL_T0PAIR)
         if (!skip) {
             if (threadIdx.x == 0) acquire_agent();
             else __builtin_amdgcn_s_dcache_inv();
             __syncthreads();
-            const CompPlan P = plans[2 * c + par];
-            if (tile == 0 && SCAN_WAVES * P.sub <= TL_STAGE_NODES)  // block-uniform
+            CompPlan P = plans[2 * c + par];
+            if (tile == 0 && (P.k0 & 2)) {  // the paired first tile: half-size block-slices (TL_T0PAIR)
+                P.sub = (P.sub + 1) / 2;
+                P.nslice *= 2;
+                unsigned* const pr = &ctl->tpair[par][c][0];
+                if (SCAN_WAVES * P.sub <= TL_STAGE_NODES)  // block-uniform
+                    counts = scan_tile_tl<true, TL_KS, true>(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu,
+                                                             jwall, jpart, cand, bnd, wjob, H, slot_min,
+                                                             xk, smem + TL_STAGE_OFF, pr);
+                else
+                    counts = scan_tile_tl<false, TL_KS, true>(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu,
+                                                              jwall, jpart, cand, bnd, wjob, H, slot_min,
+                                                              xk, nullptr, pr);
+            } else if (tile == 0 && SCAN_WAVES * P.sub <= TL_STAGE_NODES)  // block-uniform
                 scan_tile_tl<true>(P, tile, s, slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd,
                                    wjob, H, slot_min, xk, smem + TL_STAGE_OFF);
             else
@@ -1169,7 +1236,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         if (threadIdx.x == 0) {
             // the tile's outputs were written through and every storing wave waited for them
             // (vmcnt(0) above, then the barrier): the counts need no release fence (R1)
-            __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (counts)
+                __hip_atomic_fetch_add(&ctl->tdone[par][c][tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the tile count must land before the done count: once a committer sees `done` reach
             // its target it resets the tile counters for the next round, and a late increment
             // would then mark a tile of that round complete before it was scanned
