@@ -285,9 +285,10 @@ int fit_admit(fit_admitter* a, const fit_admit_req* req, fit_admit_res* res);
 /* All-or-nothing admission of n requests (the tasks of one array job, fit_pod_demand): they join
  * ONE batch, consecutively in arrival order at their own priority.  If any of them is not placed,
  * none is: every res[i].node[0] is FIT_REJECTED (some task violates the partition limits) or
- * FIT_UNPLACED, ticket 0, and what the placed ones took goes back to the table before the next
- * batch (requests after the group in the same batch saw it taken: conservative, never an
- * over-commit).  Errors as fit_admit. */
+ * FIT_UNPLACED, ticket 0, and the group takes nothing: the batch is placed again without it, so
+ * every later request of the batch sees the table the group left untouched — the sequential
+ * semantics of placing the requests one after the other (tests/test_callsite_gpu.py
+ * test_groups_in_one_batch_match_oracle).  Errors as fit_admit. */
 int fit_admit_group(fit_admitter* a, const fit_admit_req* reqs, int32_t n, fit_admit_res* res);
 /* Replaces the node table between batches (the node ticker, provider.go:470-488).  Every open
  * reservation (admitted, neither confirmed nor released) is taken from the new table again
