@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 6
+#define FITGPU_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -177,6 +177,22 @@ int fit_place_tl(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem
 int fit_place_tl_device(fit_ctx* ctx, int32_t j, const int32_t* cpu, const int32_t* mem,
                         const int32_t* gpu, const int32_t* wall, const uint16_t* part,
                         int32_t* out_node, int32_t* out_start, fit_stats* stats);
+/* Release events for fit_load_timeline from the running jobs a caller knows — the virtual
+ * kubelet's own pods: JobInfo.end_time and JobInfo.node_list (workload.proto:252-292; the
+ * node_list expanded with fit_expand_hostlist and mapped to engine rows through the
+ * fit_node_names table) and each pod's per-node demand (fit_pod_demand).  Job i holds (cpu[i],
+ * mem[i], gpu[i]) on every node job_nodes[job_off[i] .. job_off[i+1]) for rem_min[i] more minutes
+ * (end_time − now) and hands it back at slot max(1, ceil(rem_min / slot_min)), capped at `slots`
+ * (a job past its end time holds its nodes until Slurm ends it; a release at the horizon changes
+ * nothing).  Output: the CSR by node fit_load_timeline reads (rel_off[n + 1]; rel_slot / rel_cpu /
+ * rel_mem / rel_gpu, slots non-decreasing per node, jobs in order within a slot), at most cap
+ * events.  Returns the event count or FIT_E_INVAL (node id out of range, negative demand,
+ * job_off not starting at 0 or decreasing, slots / slot_min < 1, cap too small). */
+int fit_release_events(int32_t n, int32_t m, const int32_t* job_off, const int32_t* job_nodes,
+                       const int64_t* rem_min, const int32_t* cpu, const int32_t* mem,
+                       const int32_t* gpu, int32_t slots, int32_t slot_min, int32_t* rel_off,
+                       int32_t* rel_slot, int32_t* rel_cpu, int32_t* rel_mem, int32_t* rel_gpu,
+                       int32_t cap);
 /* Current timelines, dense [n][slots] per column, host pointers (n * slots entries each).  Slots
  * where a node is unusable, and nodes outside every partition, read -1. */
 int fit_read_timeline(fit_ctx* ctx, int32_t* cpu, int32_t* mem, int32_t* gpu);

@@ -821,4 +821,51 @@ int fit_node_columns(const fit_node* nodes, int32_t n, uint32_t part_mask, int32
     return n;
 }
 
+int fit_release_events(int32_t n, int32_t m, const int32_t* job_off, const int32_t* job_nodes,
+                       const int64_t* rem_min, const int32_t* cpu, const int32_t* mem,
+                       const int32_t* gpu, int32_t slots, int32_t slot_min, int32_t* rel_off,
+                       int32_t* rel_slot, int32_t* rel_cpu, int32_t* rel_mem, int32_t* rel_gpu,
+                       int32_t cap) {
+    if (n < 0 || m < 0 || slots < 1 || slot_min < 1 || cap < 0 || !rel_off ||
+        (m > 0 && (!job_off || !rem_min || !cpu || !mem || !gpu)))
+        return FIT_E_INVAL;
+    if (m > 0 && job_off[0] != 0) return FIT_E_INVAL;
+    for (int32_t i = 0; i < m; ++i)
+        if (job_off[i + 1] < job_off[i] || cpu[i] < 0 || mem[i] < 0 || gpu[i] < 0) return FIT_E_INVAL;
+    const int32_t e = m > 0 ? job_off[m] : 0;
+    if (e > 0 && !job_nodes) return FIT_E_INVAL;
+    if (e > cap || (e > 0 && (!rel_slot || !rel_cpu || !rel_mem || !rel_gpu))) return FIT_E_INVAL;
+    // one event per (job, node): node, slot, job — ordered by node, then slot, then job order
+    struct Ev {
+        int32_t node, slot, job;
+    };
+    std::vector<Ev> ev;
+    ev.reserve((size_t)e);
+    for (int32_t i = 0; i < m; ++i) {
+        // minutes left → the slot whose start the release reaches: ceil(rem / slot_min), at least
+        // 1 (a job past its end time holds its nodes until Slurm ends it), capped at the horizon
+        const int64_t r = rem_min[i] <= 0 ? 1 : (rem_min[i] + slot_min - 1) / slot_min;
+        const int32_t sl = (int32_t)std::min<int64_t>(std::max<int64_t>(r, 1), slots);
+        for (int32_t k = job_off[i]; k < job_off[i + 1]; ++k) {
+            const int32_t x = job_nodes[k];
+            if (x < 0 || x >= n) return FIT_E_INVAL;
+            ev.push_back(Ev{x, sl, i});
+        }
+    }
+    std::stable_sort(ev.begin(), ev.end(), [](const Ev& a, const Ev& b) {
+        return a.node != b.node ? a.node < b.node : a.slot < b.slot;
+    });
+    std::fill(rel_off, rel_off + n + 1, 0);
+    for (const Ev& v : ev) ++rel_off[v.node + 1];
+    for (int32_t x = 0; x < n; ++x) rel_off[x + 1] += rel_off[x];
+    for (int32_t k = 0; k < e; ++k) {
+        const Ev& v = ev[(size_t)k];
+        rel_slot[k] = v.slot;
+        rel_cpu[k] = cpu[v.job];
+        rel_mem[k] = mem[v.job];
+        rel_gpu[k] = gpu[v.job];
+    }
+    return e;
+}
+
 }  // extern "C"

@@ -145,6 +145,26 @@ def node_names(entries: list[str]) -> list[str]:
         buflen *= 16
 
 
+def release_events(n: int, jobs: list, slots: int, slot_min: int):
+    """Release events for Engine.load_timeline from running jobs (fit_release_events): ``jobs`` is a
+    list of (node rows, minutes left, cpu, mem MiB, gpus); returns a synth.Timeline."""
+    from .synth import Timeline
+    m = len(jobs)
+    off = np.zeros(m + 1, np.int32)
+    for i, j in enumerate(jobs):
+        off[i + 1] = off[i] + len(j[0])
+    nodes = np.array([x for j in jobs for x in j[0]], np.int32)
+    rem = np.array([j[1] for j in jobs], np.int64)
+    cols = [np.array([j[k] for j in jobs], np.int32) for k in (2, 3, 4)]
+    e = int(off[-1])
+    out = [np.zeros(n + 1, np.int32)] + [np.zeros(max(e, 1), np.int32) for _ in range(4)]
+    r = lib().fit_release_events(n, m, _ptr(off), _ptr(nodes) if e else None, _ptr(rem), *[_ptr(c) for c in cols],
+                                 slots, slot_min, *[_ptr(o) for o in out], e)
+    check(r, "fit_release_events")
+    return Timeline(slots=slots, slot_min=slot_min, off=out[0], slot=out[1][:r], cpu=out[2][:r],
+                    mem=out[3][:r], gpu=out[4][:r])
+
+
 def ingest_nodes(text: str, partitions: list[str]):
     """`scontrol show nodes` text → (synth.Nodes columns for Engine.load_nodes, node names)
     (Client.Nodes + parseNode, slurm.go:354-363 / parse.go:291-308, plus Gres,

@@ -39,7 +39,7 @@ EXPORTS = [
     "fit_admitter_reservations", "fit_admitter_pending", "fit_admitter_destroy",
     "fit_array_tasks", "fit_pod_demand", "fit_script_with_nodelist", "fit_partition_limits",
     "fit_node_columns", "fit_node_names", "fit_admitter_load_table", "fit_admitter_generation",
-    "fit_admitter_script", "fit_set_max_array_size",
+    "fit_admitter_script", "fit_set_max_array_size", "fit_release_events",
 ]
 
 
@@ -173,6 +173,7 @@ def lib() -> C.CDLL:
         L.fit_admitter_script.argtypes = [P, C.POINTER(i64), i32, C.c_char_p, C.c_char_p, i32, C.POINTER(i32)]
         L.fit_set_max_array_size.argtypes = [i32]
         L.fit_set_max_array_size.restype = i32
+        L.fit_release_events.argtypes = [i32, i32, P, P, P, P, P, P, i32, i32, P, P, P, P, P, i32]
         L.fit_parse_duration.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.fit_parse_resources.argtypes = [C.c_char_p, C.POINTER(FitResources)]
         L.fit_parse_nodes.argtypes = [C.c_char_p, C.POINTER(FitNode), i32]

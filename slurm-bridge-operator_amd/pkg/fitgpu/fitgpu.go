@@ -184,6 +184,51 @@ func (e *Engine) LoadTimeline(slots, slotMin int, r Releases) error {
 		(*C.int32_t)(unsafe.Pointer(&r.Off[0])), s, c, m, g))
 }
 
+// RunningJob is one job the caller knows is running (the virtual kubelet's own pods): its engine
+// node rows (JobInfo.node_list expanded with ExpandHostlist, mapped through the NodeNames table),
+// the minutes left until JobInfo.end_time (workload.proto:252-292) and its per-node demand.
+type RunningJob struct {
+	Nodes            []int32
+	MinutesLeft      int64
+	CPU, MemMiB, GPU int32
+}
+
+// ReleaseEvents turns running jobs into the release events LoadTimeline reads
+// (fit_release_events): each job hands its demand back on each of its nodes at slot
+// max(1, ceil(MinutesLeft / slotMin)), capped at the horizon.
+func ReleaseEvents(nodes int, jobs []RunningJob, slots, slotMin int) (Releases, error) {
+	off := make([]int32, len(jobs)+1)
+	var rows []int32
+	rem := make([]int64, len(jobs))
+	cpu, mem, gpu := make([]int32, len(jobs)), make([]int32, len(jobs)), make([]int32, len(jobs))
+	for i, j := range jobs {
+		rows = append(rows, j.Nodes...)
+		off[i+1] = int32(len(rows))
+		rem[i], cpu[i], mem[i], gpu[i] = j.MinutesLeft, j.CPU, j.MemMiB, j.GPU
+	}
+	e := len(rows)
+	r := Releases{Off: make([]int32, nodes+1), Slot: make([]int32, e), CPU: make([]int32, e),
+		MemMiB: make([]int32, e), GPU: make([]int32, e)}
+	p32 := func(v []int32) *C.int32_t {
+		if len(v) == 0 {
+			return nil
+		}
+		return (*C.int32_t)(unsafe.Pointer(&v[0]))
+	}
+	var remp *C.int64_t
+	if len(rem) > 0 {
+		remp = (*C.int64_t)(unsafe.Pointer(&rem[0]))
+	}
+	n := C.fit_release_events(C.int32_t(nodes), C.int32_t(len(jobs)), p32(off), p32(rows), remp, p32(cpu),
+		p32(mem), p32(gpu), C.int32_t(slots), C.int32_t(slotMin), p32(r.Off), p32(r.Slot), p32(r.CPU),
+		p32(r.MemMiB), p32(r.GPU), C.int32_t(e))
+	runtime.KeepAlive(rows)
+	if err := check(n); err != nil {
+		return Releases{}, err
+	}
+	return r, nil
+}
+
 // PlaceBackfill gives each job (one node) its node and earliest start slot (DESIGN.md §2b);
 // node is Unplaced when nothing fits inside the horizon, Rejected for partition limits.
 func (e *Engine) PlaceBackfill(j Jobs) (node, start []int32, st Stats, err error) {
