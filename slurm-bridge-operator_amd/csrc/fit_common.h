@@ -166,6 +166,37 @@ __device__ __forceinline__ void store_job(JobRec* dst, const JobRec& J) {
     }
 }
 
+// The persistent engines' candidate lists, written through with the whole block: wave 0 (lane =
+// job) puts its KW keys into LDS (`buf`, KW * 64 u64), then thread i stores 16 B of job i / (KW/2)
+// with one sc1 dwordx4 store, so 8 (KW = 16) or 2 (KW = 4) consecutive lanes write a job's
+// contiguous list — whole 64-B lines instead of KW separate 8-B partial writes per lane (the
+// fabric counts each partial write: C3 wrote 3.7 GB per launch that way).  Every thread of the
+// block calls it (one barrier inside); each storing wave drains its stores before the caller's
+// tile count, as before.
+#ifndef FIT_COALESCED_LISTS
+#define FIT_COALESCED_LISTS 1
+#endif
+template <int KW>
+__device__ __forceinline__ void store_lists_through(uint64_t* __restrict__ buf, bool wave0, int lane,
+                                                    const uint64_t* key, int nkey, uint64_t* base,
+                                                    int64_t job_stride, int nactive) {
+    static_assert(KW % 2 == 0, "16-B chunks");
+    if (wave0) {
+#pragma unroll
+        for (int i = 0; i < KW; ++i) buf[lane * KW + i] = i < nkey ? key[i] : KEY_INF;
+    }
+    __syncthreads();
+    constexpr int CPJ = KW / 2;  // 16-B chunks per job
+    for (int i = threadIdx.x; i < 64 * CPJ; i += SCAN_WAVES * 64) {
+        const int j = i / CPJ, c = i - j * CPJ;
+        if (j >= nactive) break;  // i only grows
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        const v4 v = *reinterpret_cast<const v4*>(buf + j * KW + 2 * c);
+        uint64_t* dst = base + j * job_stride + 2 * c;
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+    }
+}
+
 // -------------------------------------------------------------------------------- k_scan
 // Block = SCAN_JOBS jobs (lanes) × one block-slice of SCAN_WAVES sub-slices (one per wave).
 // Each wave keeps the exact top-K of its sub-slice; the 8 lists are merged through LDS in a
@@ -295,6 +326,19 @@ __device__ __forceinline__ bool scan_tile(
     if (feas != nullptr && wave == 0) {  // the tile's jobs with a fitting node in this block-slice
         const uint64_t fm = __ballot(active && key[0] != KEY_INF);
         if (lane == 0 && fm != 0ull) atomicOr(feas, (unsigned long long)fm);
+    }
+    if constexpr (PERSISTENT && !PAIR && FIT_COALESCED_LISTS) {
+        // every thread: the lists through LDS (the merge buffer, free again) and out coalesced
+        const int na = max(0, min(SCAN_JOBS, P.w - tile * SCAN_JOBS));
+        store_lists_through<KW>(reinterpret_cast<uint64_t*>(xk), wave == 0, lane, key, K,
+                                cand + P.cand_off + ((int64_t)(tile * SCAN_JOBS) * P.nslice + s) * KW,
+                                (int64_t)P.nslice * KW, na);
+        if (wave != 0 || !active) return true;
+        if (key[K - 1] != KEY_INF)
+            atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
+                      (unsigned long long)key[K - 1]);
+        if (s == 0) store_job<PERSISTENT>(wjob + P.slot0 + t, J);
+        return true;
     }
     if (wave != 0) return true;  // (no barrier follows inside scan_tile)
     if constexpr (PAIR) {

@@ -377,6 +377,19 @@ __device__ __forceinline__ bool scan_tile_tl(
         }
         __syncthreads();
     }
+    if constexpr (!PAIR && FIT_COALESCED_LISTS) {
+        // every thread: the lists out through LDS, coalesced (store_lists_through, fit_common.h)
+        const int na = max(0, min(SCAN_JOBS, P.w - tile * SCAN_JOBS));
+        store_lists_through<K>(reinterpret_cast<uint64_t*>(xk), wave == 0, lane, key, K,
+                               cand + P.cand_off + ((int64_t)(tile * SCAN_JOBS) * P.nslice + s) * K,
+                               (int64_t)P.nslice * K, na);
+        if (wave != 0 || !active) return true;
+        if (key[K - 1] != KEY_INF)
+            atomicMin(reinterpret_cast<unsigned long long*>(bnd + P.slot0 + t),
+                      (unsigned long long)key[K - 1]);
+        if (s == 0) store_job<true>(wjob + P.slot0 + t, J);
+        return true;
+    }
     if (wave != 0) return true;
     if constexpr (PAIR) {
         const int ns = P.nslice >> 1, pr = s >> 1;
