@@ -497,6 +497,8 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
+    // every bound KEY_INF: a round resets only the bounds its buffer set's last round used
+    HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * 2 * nc * wcap, st));
     HIP_TRY(hipEventRecord(c->ev[0], st));
     HIP_TRY(launch_engine(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
                           c->plan.p, nc, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
@@ -815,6 +817,8 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
+    // every bound KEY_INF: a round resets only the bounds its buffer set's last round used
+    HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * 2 * nc * wcap, st));
     HIP_TRY(hipEventRecord(c->ev[0], st));
     bool resident_late = false;
     if (!split) {

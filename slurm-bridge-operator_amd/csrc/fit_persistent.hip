@@ -67,6 +67,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         MwShared* M = reinterpret_cast<MwShared*>(smem);
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity
+        // job tiles published by the last round of each parity: only their bounds can differ from
+        // KEY_INF (the host sets them all before the launch), so only those are reset
+        unsigned used[2] = {0u, 0u};
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         bool prev_multi = false;  // the previous round ran the single-wave commit (plain row stores)
         while (cursor < S.jend) {
@@ -108,7 +111,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 // just in time need no release of their own (R1: stored, drained, then the
                 // block barrier, then their task stores)
                 store_through(&plans[2 * c + par], P);
-                for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
+                const int nres = min((int)used[par] * SCAN_JOBS, S.wmax);  // within the slot region
+                for (int i = lane; i < nres; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64) {
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&ctl->tfeas[par][c][i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -184,6 +188,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 R = CommitResult{M->res[0], M->res[1], M->res[2], M->res[3]};
                 __syncthreads();
             }
+            if (wave == 0) used[par] = M->pubt;  // stable after the commit's closing barrier
             if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
             if (R.stop == 3) {  // commit watchdog
                 if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);

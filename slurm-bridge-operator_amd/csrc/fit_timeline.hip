@@ -1049,6 +1049,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const CompState S = cs[c];
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity (fit_engine_ctl.h)
+        unsigned used[2] = {0u, 0u};    // job tiles whose bounds the last round of each parity reset
+                                        // and its scans lowered (k_engine's, fit_persistent.hip)
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         bool fail = false;
         bool glob = false;  // the last window wrote a global-slab list (plain stores)
@@ -1080,7 +1082,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 bool f = !wait_tiles(ctl, c, par, target[par]);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 store_through(&plans[2 * c + par], P);  // as k_engine's (fit_persistent.hip)
-                for (int i = lane; i < w; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
+                const int nres = min((int)used[par] * SCAN_JOBS, S.wmax);  // within the slot region
+                for (int i = lane; i < nres; i += 64) store_through64(&bnd[P.slot0 + i], KEY_INF);
                 for (unsigned i = lane; i < ntj; i += 64)
                     __hip_atomic_store(&ctl->tdone[par][c][i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (lane < 32) __hip_atomic_store(&ctl->tpair[par][c][lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1125,8 +1128,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             // every tile published this round (the committer's and the helpers') must be complete
             // before the next round reuses the buffers: count them (pubt is stable after the
             // commit's closing barrier)
-            if (wave == 0)
+            if (wave == 0) {
                 target[par] += (reinterpret_cast<TmShared*>(smem)->pubt + ((P.k0 & 2) ? 1u : 0u)) * (unsigned)S.nslice;
+                used[par] = reinterpret_cast<TmShared*>(smem)->pubt;
+            }
             if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
             if (r.stop == 3) {
                 fail = true;
