@@ -35,6 +35,9 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
 #ifndef FIT_K0
 #define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
 #endif
+#ifndef K_T0PAIR4
+#define K_T0PAIR4 1  // ... also a 4-key component's (C3o: one 100k-node component, 32 slices x 4 keys)
+#endif
 #ifndef K_T0PAIR
 #define K_T0PAIR 1  // k_engine: a k = 1 window's first job tile as 2 x nslice half-size block-slices, paired
 #endif
@@ -96,7 +99,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             const bool multi = jpk[cursor + w] != jpk[cursor];
             // a multi-node job needs k <= KS keys in its first tile; a k = 1 window's first tile
             // keeps FIT_K0 keys per block-slice and is scanned as paired half-slices (K_T0PAIR)
-            const bool pair = !multi && K_T0PAIR && 2 * S.nslice <= 64 && FIT_K0 > 0 && FIT_K0 < S.ks;
+            // (the pair scratch holds 4 keys: the FIT_K0 list, or a 4-key component's own, C3o)
+            const bool pair = !multi && K_T0PAIR && 2 * S.nslice <= 64 &&
+                              ((FIT_K0 > 0 && FIT_K0 < S.ks) || (K_T0PAIR4 && S.ks <= 4));
             P.k0 = multi ? 0 : (1 | (pair ? 2 : 0));
             P.pair_off = S.pair_off + (par ? PAIR_AREA : 0);
             MW_CLK(rs0);
@@ -300,6 +305,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             else                                                                                  \
                 scan_tile<true, K0_, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, \
                                          cand, bnd, wjob, xk0, &ctl->tfeas[par][c][tile]);             \
+        } else if (K_ <= 4 && pair) { /* a 4-key component's first tile, paired */               \
+            if constexpr (K_ <= 4) {                                                              \
+                uint64_t(*xk4)[K_][64] = reinterpret_cast<uint64_t(*)[K_][64]>(smem);             \
+                if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                         \
+                    counts = scan_tile<true, K_, K_, true, true>(                                 \
+                        P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk4, \
+                        &ctl->tfeas[par][c][tile], reinterpret_cast<NodeRec*>(smem + STAGE_OFF),     \
+                        &ctl->tpair[par][c][0]);                                                  \
+                else                                                                              \
+                    counts = scan_tile<true, K_, K_, false, true>(                                \
+                        P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk4, \
+                        &ctl->tfeas[par][c][tile], nullptr, &ctl->tpair[par][c][0]);              \
+            }                                                                                     \
         } else {                                                                                  \
             scan_tile<true, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand,    \
                                 bnd, wjob, reinterpret_cast<uint64_t(*)[K_][64]>(smem),           \
