@@ -97,10 +97,12 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5", "admit"],
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5", "c2a", "c3a", "c5a", "admit"],
                     help="c3: BASELINE headline (100k x 1M); c3o: c3 + an all-nodes partition (one "
                          "component); c5: c3 with a 1,024-slot backfill horizon; admit: CreatePod "
-                         "admission latency (10 concurrent callers against the c3 node table)")
+                         "admission latency (10 concurrent callers against the c3 node table); c2a / c3a / "
+                         "c5a: the same clusters with an array-expanded pending queue (runs of identical "
+                         "pods, synth.expand_arrays) — not a BASELINE config")
     ap.add_argument("--repeats", type=int, default=3,
                     help="timed runs of --steps steps each; value = their median (BASELINE.md:26)")
     ap.add_argument("--no-shard-price", action="store_true",
@@ -172,8 +174,13 @@ def main():
     shard = rank if weak else 0  # weak: this rank's own cluster shard (disjoint generator slice)
 
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
-    tl = a.workload == "c5"
-    if tl:
+    tl = a.workload in ("c5", "c5a")
+    if a.workload.endswith("a"):
+        if shard:
+            raise SystemExit("array-expanded workloads: strong scaling or one GPU only")
+        cfg = synth.make_array_config(a.workload)
+        nodes, tline, jobs, parts = cfg if tl else (cfg[0], None, cfg[1], cfg[2])
+    elif tl:
         nodes, tline, jobs, parts = synth.make_c5(shard=shard)
     else:
         nodes, jobs, parts = synth.make_config(a.workload, shard=shard)

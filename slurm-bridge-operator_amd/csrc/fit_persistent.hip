@@ -35,6 +35,14 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
 #ifndef FIT_K0
 #define FIT_K0 4  // > 0: a round's first job tile keeps FIT_K0 keys per block-slice (scan_tile KW)
 #endif
+#ifndef FIT_K0W
+#define FIT_K0W 8  // > 0: the first job tile after a rescan inside the previous round's first tile keeps
+                   // FIT_K0W keys per block-slice, unpaired, for K0W_ROUNDS rounds ("wide"): runs of
+                   // identical jobs (array tasks) drain the FIT_K0 lists' bound within a few jobs
+#endif
+#ifndef K0W_ROUNDS
+#define K0W_ROUNDS 8
+#endif
 #ifndef K_T0PAIR4
 #define K_T0PAIR4 1  // ... also a 4-key component's (C3o: one 100k-node component, 32 slices x 4 keys)
 #endif
@@ -75,6 +83,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         unsigned used[2] = {0u, 0u};
         int64_t evals = 0, placed = 0, rounds = 0, sr = 0, sd = 0, tc = 0, tw = 0;
         bool prev_multi = false;  // the previous round ran the single-wave commit (plain row stores)
+        int wide_left = 0;        // rounds left whose first tile is wide (FIT_K0W)
         while (cursor < S.jend) {
             const int w = min(win, S.jend - cursor);
             const unsigned rnd = (unsigned)rounds + 1u;  // task round tag
@@ -100,9 +109,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             // a multi-node job needs k <= KS keys in its first tile; a k = 1 window's first tile
             // keeps FIT_K0 keys per block-slice and is scanned as paired half-slices (K_T0PAIR)
             // (the pair scratch holds 4 keys: the FIT_K0 list, or a 4-key component's own, C3o)
-            const bool pair = !multi && K_T0PAIR && 2 * S.nslice <= 64 &&
-                              ((FIT_K0 > 0 && FIT_K0 < S.ks) || (K_T0PAIR4 && S.ks <= 4));
-            P.k0 = multi ? 0 : (1 | (pair ? 2 : 0));
+            // — unless a recent round stopped for a rescan inside its first tile: then FIT_K0W keys
+            // per block-slice, unpaired (bit 2; components with ks <= FIT_K0W keep their first tile)
+            const bool wide = !multi && FIT_K0W > 0 && FIT_K0W < S.ks && wide_left > 0;
+            const bool pair = !multi && !wide && K_T0PAIR && 2 * S.nslice <= 64 &&
+                              ((FIT_K0 > 0 && FIT_K0 <= 4 && FIT_K0 < S.ks) || (K_T0PAIR4 && S.ks <= 4));
+            P.k0 = multi ? 0 : wide ? 4 : (1 | (pair ? 2 : 0));
             P.pair_off = S.pair_off + (par ? PAIR_AREA : 0);
             MW_CLK(rs0);
             if (wave == 0) {
@@ -212,6 +224,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             ++rounds;
             sr += R.stop == 1;
             sd += R.stop == 2;
+            if (R.stop == 1 && R.done < SCAN_JOBS) wide_left = K0W_ROUNDS;
+            else if (wide_left > 0) --wide_left;
             cursor += R.done;
 #ifndef ENGINE_WGROW
 #define ENGINE_WGROW 10  // next window after a stop, in eighths of the jobs the round resolved
@@ -286,19 +300,34 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             switch (P.ks) {  // block-uniform; the host picks one of these (engine.cpp)
 #define SCAN_K(K_)                                                                               \
     case K_:                                                                                      \
-        if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && P.k0) {                                     \
+        if (FIT_K0W > 0 && FIT_K0W < K_ && tile == 0 && (P.k0 & 4)) { /* wide, unpaired */          \
+            constexpr int KW_ = (FIT_K0W > 0 && FIT_K0W < K_ ? FIT_K0W : K_);                        \
+            uint64_t(*xkw)[KW_][64] = reinterpret_cast<uint64_t(*)[KW_][64]>(smem);                 \
+            if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                               \
+                scan_tile<true, KW_, K_, true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart,   \
+                                               jk, cand, bnd, wjob, xkw, &ctl->tfeas[par][c][tile],    \
+                                               reinterpret_cast<NodeRec*>(smem + STAGE_OFF));     \
+            else                                                                                  \
+                scan_tile<true, KW_, K_>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, \
+                                         cand, bnd, wjob, xkw, &ctl->tfeas[par][c][tile]);             \
+        } else if (FIT_K0 > 0 && FIT_K0 < K_ && tile == 0 && (P.k0 & 1)) {                        \
             constexpr int K0_ = (FIT_K0 > 0 && FIT_K0 < K_ ? FIT_K0 : K_);                        \
             uint64_t(*xk0)[K0_][64] = reinterpret_cast<uint64_t(*)[K0_][64]>(smem);               \
-            if (pair && SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                      \
-                counts = scan_tile<true, K0_, K_, true, true>(                                    \
-                    P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0,   \
-                    &ctl->tfeas[par][c][tile], reinterpret_cast<NodeRec*>(smem + STAGE_OFF),         \
-                    &ctl->tpair[par][c][0]);                                                      \
-            else if (pair)                                                                        \
-                counts = scan_tile<true, K0_, K_, false, true>(                                   \
-                    P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0,   \
-                    &ctl->tfeas[par][c][tile], nullptr, &ctl->tpair[par][c][0]);                  \
-            else if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                         \
+            bool done_ = false;                                                                   \
+            if constexpr (K0_ <= 4) { /* the pair scratch holds 4 keys */                          \
+                done_ = pair;                                                                     \
+                if (pair && SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                  \
+                    counts = scan_tile<true, K0_, K_, true, true>(                                \
+                        P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0, \
+                        &ctl->tfeas[par][c][tile], reinterpret_cast<NodeRec*>(smem + STAGE_OFF),     \
+                        &ctl->tpair[par][c][0]);                                                  \
+                else if (pair)                                                                    \
+                    counts = scan_tile<true, K0_, K_, false, true>(                               \
+                        P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, xk0, \
+                        &ctl->tfeas[par][c][tile], nullptr, &ctl->tpair[par][c][0]);              \
+            }                                                                                     \
+            if (done_) {                                                                          \
+            } else if (SCAN_WAVES * P.sub <= STAGE_ROWS) /* block-uniform */                       \
                 scan_tile<true, K0_, K_, true>(P, tile, s, rec, jl, jcpu, jmem, jgpu, jwall, jpart, \
                                                jk, cand, bnd, wjob, xk0, &ctl->tfeas[par][c][tile],    \
                                                reinterpret_cast<NodeRec*>(smem + STAGE_OFF));     \

@@ -30,6 +30,7 @@ S_RN, S_RS = 9, 10  # C5: running jobs per node, their release slots
 S_JCPU, S_JMEM, S_JGPUF, S_JGPUV, S_JWO, S_JWV, S_JPART, S_JK = range(16, 24)
 S_PTIME = 32
 S_JALL = 24  # c3o: job targets the all-nodes partition
+S_ARUN = 25  # array-expanded streams: tasks per array job
 
 NODE_CPUS = np.array([32, 64, 96, 128, 192, 256], dtype=np.int64)
 NODE_MEMMUL = np.array([2048, 4096, 8192], dtype=np.int64)
@@ -236,6 +237,39 @@ def make_config(name: str, nodes: int | None = None, jobs: int | None = None, sh
     i = np.arange(shard * j, shard * j + j, dtype=np.uint64)
     jb.part = np.where(uni(rnd(seed, S_JALL, i), 100) < C3O_ALL_PCT, p, jb.part).astype(np.uint16)
     return nd, jb, gen_partitions(seed, p + 1)
+
+
+# Array-expanded streams: `--array=1-N` turns one SlurmBridgeJob into N
+# identical pods (fit_array_tasks; reference pkg/slurm-bridge-operator/parse.go array handling), so
+# the pending queue holds runs of identical demands.  Tasks per array job from ARRAY_RUNS.
+ARRAY_RUNS = np.array([1, 1, 2, 4, 8, 8, 16, 32], dtype=np.int64)
+
+
+def expand_arrays(seed: int, jobs: Jobs, j: int | None = None) -> Jobs:
+    """The first ``j`` (default: as many as ``jobs``) pods of the stream in which job i of ``jobs``
+    is an array job of ARRAY_RUNS[u] identical tasks, each task its own pending pod in priority
+    order (mean 9 tasks per array job)."""
+    j = jobs.j if j is None else j
+    runs = ARRAY_RUNS[uni(rnd(seed, S_ARUN, np.arange(jobs.j, dtype=np.uint64)), len(ARRAY_RUNS))]
+    src = np.repeat(np.arange(jobs.j), runs)[:j]
+    if len(src) < j:
+        raise ValueError(f"expand_arrays: {jobs.j} array jobs give {len(src)} < {j} pods")
+    return Jobs(cpu=jobs.cpu[src], mem=jobs.mem[src], gpu=jobs.gpu[src], wall=jobs.wall[src],
+                part=jobs.part[src], nodes_k=jobs.nodes_k[src])
+
+
+def make_array_config(name: str, nodes: int | None = None, jobs: int | None = None):
+    """``name`` in c2a / c3a / c5a: config c2 / c3 / c5's cluster with an array-expanded pending
+    queue of the same length.  Returns make_config's (or make_c5's) tuple."""
+    base = name[:-1]
+    n, j, _p, _gh, _mn = CONFIGS[base]
+    j = j if jobs is None else jobs
+    seed = SEEDS[base]
+    if base == "c5":
+        nd, tl, jb, pt = make_c5(nodes, j // 4 + 64)
+        return nd, tl, expand_arrays(seed, jb, j), pt
+    nd, jb, pt = make_config(base, nodes, j // 4 + 64)
+    return nd, expand_arrays(seed, jb, j), pt
 
 
 def make_c5(nodes: int | None = None, jobs: int | None = None, shard: int = 0):

@@ -1,11 +1,12 @@
-"""Full-size golden digests for BASELINE configs C4 and C5 (run offline in the dev container).
+"""Full-size golden digests for BASELINE configs C4 and C5 (run offline in the dev container), and
+for their array-expanded streams c3a / c4a / c5a (synth.make_array_config).
 
 C5 (100k nodes x 1M jobs, 1,024-slot horizon) takes the oracle (oracle/fitref_tl.c:ref_place_tl,
 dense timelines, one thread) about 1.5 h; C4 (100k GPU-heavy nodes x 1M multi-node jobs, kmax 8)
 runs oracle/fitref.c:ref_place.  The digests land in tests/golden/placements_big.json and are
 checked by tests/test_golden_big_gpu.py.
 
-    python tools/make_golden_big.py c4|c5
+    python tools/make_golden_big.py c4|c5|c3a|c4a|c5a
 """
 import hashlib
 import json
@@ -35,29 +36,31 @@ def save(key, rec):
     print(key, rec, flush=True)
 
 
-def c5():
+def c5(name="c5"):
     from fitgpu import synth
     from oracle import pyoracle as po
-    nodes, tline, jobs, parts = synth.make_c5()
+    nodes, tline, jobs, parts = synth.make_c5() if name == "c5" else synth.make_array_config(name)
     t = time.time()
     node, start, st, tl = po.ref_place_tl(nodes, tline, jobs, parts)
-    save(f"c5:{nodes.n}x{jobs.j}", {
+    save(f"{name}:{nodes.n}x{jobs.j}", {
         "node_sha256": sha(node), "start_sha256": sha(start),
         "final_cpu_sha256": sha(tl[..., 0]), "final_mem_sha256": sha(tl[..., 1]),
         "final_gpu_sha256": sha(tl[..., 2]), **st, "oracle_seconds": round(time.time() - t, 1)})
 
 
-def c4():
+def c4(name="c4"):
     from fitgpu import synth
     from oracle import pyoracle as po
-    nodes, jobs, parts = synth.make_config("c4")
+    nodes, jobs, parts = synth.make_config(name) if name in ("c3", "c4") else synth.make_array_config(name)
+    kmax = 8 if name.startswith("c4") else 1
     t = time.time()
-    out, st, fin = po.ref_place(nodes, jobs, parts, kmax=8)
-    save(f"c4:{nodes.n}x{jobs.j}", {
-        "kmax": 8, "placements_sha256": sha(out), "final_cpu_sha256": sha(fin[0]),
+    out, st, fin = po.ref_place(nodes, jobs, parts, kmax=kmax)
+    save(f"{name}:{nodes.n}x{jobs.j}", {
+        "kmax": kmax, "placements_sha256": sha(out), "final_cpu_sha256": sha(fin[0]),
         "final_mem_sha256": sha(fin[1]), "final_gpu_sha256": sha(fin[2]), **st,
         "oracle_seconds": round(time.time() - t, 1)})
 
 
 if __name__ == "__main__":
-    {"c4": c4, "c5": c5}[sys.argv[1]]()
+    n = sys.argv[1]
+    (c5 if n.startswith("c5") else c4)(n)
