@@ -12,7 +12,7 @@ from fitgpu import Engine, synth  # noqa: E402
 
 W = 24  # stamps per component (MW_NSTAMP)
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
-nodes, jobs, parts = synth.make_config(name)
+nodes, jobs, parts = synth.make_array_config(name) if name.endswith("a") else synth.make_config(name)
 with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
