@@ -66,7 +66,8 @@ struct alignas(16) CompPlan {
     int64_t cand_off;    // u64 offset of the component's candidates inside one rank section
     int32_t slot0;       // first window slot (global over components)
     int32_t k0;          // persistent engines, the round's first job tile: bit 0 keeps FIT_K0 keys
-                         // (k_engine, k = 1 window); bit 1 scans it as paired half-slices (*_T0PAIR)
+                         // (k_engine, k = 1 window); bit 1 scans it as paired half-slices (*_T0PAIR);
+                         // bit 2 keeps FIT_K0W keys, unpaired (k_engine, after a first-tile rescan)
     int32_t pair_off;    // u64 offset of the round's half-slice list scratch (bit 1 of k0)
 };
 
