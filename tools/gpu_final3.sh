@@ -1,0 +1,4 @@
+set -o pipefail
+bash tools/gpu_final.sh r04f || exit 1
+FITGPU_STAMPS_LIB=$PWD/slurm-bridge-operator_amd/fitgpu/libfitgpu_tlfine.so timeout -k 10 300 python -u tools/tl_stamps.py > gpurun_out/r04f_c5_tlfine.txt 2>&1 || { tail -20 gpurun_out/r04f_c5_tlfine.txt; exit 1; }
+grep -v "comp " gpurun_out/r04f_c5_tlfine.txt
