@@ -405,6 +405,7 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         int n = 0;
 #pragma unroll
         for (int i = 0; i < TM_M; ++i) {
+            if (i >= nmax) break;  // uniform: a record needs nmax items at most
             const uint32_t hh = (uint32_t)(q[0] >> 32), ll = (uint32_t)q[0];
             const uint32_t mh = wave_min32_all(hh);
             const uint32_t ml = wave_min32_all(hh == mh ? ll : 0xffffffffu);
