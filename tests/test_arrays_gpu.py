@@ -86,3 +86,15 @@ def test_array_full_digest_backfill():
     assert sha(node) == g["node_sha256"] and sha(start) == g["start_sha256"]
     assert [sha(tl[..., i]) for i in range(3)] == [g["final_cpu_sha256"], g["final_mem_sha256"],
                                                    g["final_gpu_sha256"]]
+
+
+def test_wide_first_tile_cuts_rounds():
+    """A run of identical jobs drains a 4-key first tile's bound within a few jobs (a rescan inside
+    the first tile); k_engine then scans the next rounds' first tiles with FIT_K0W keys (DESIGN.md
+    §3.6). c2a: 79 rounds without it, 47 with it (profiles/r04_arrays_firsttile_ab.txt) — and the
+    placements stay the oracle's."""
+    nodes, jobs, parts = synth.make_array_config("c2a")
+    out, st, _ = _place(nodes, jobs, parts)
+    assert st["rounds"] <= 60, st
+    ref, _, _ = po.ref_place(nodes, jobs, parts)
+    assert np.array_equal(out, ref)
