@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FITGPU_ABI_VERSION 7
+#define FITGPU_ABI_VERSION 8
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define FIT_OK 0
@@ -103,6 +103,8 @@ typedef struct {
     int32_t components;    /* independent partition components                               */
     int32_t engine;        /* 1: persistent single-launch engine (k_engine); 0: host-driven rounds */
     int32_t reserved;
+    double ms_arb_wait;    /* host time waiting for the device's persistent-launch lock: one   */
+                           /* persistent launch per GPU at a time, across contexts and processes */
 } fit_stats;
 
 /* ---- engine -------------------------------------------------------------------------- */
@@ -113,6 +115,14 @@ const char* fit_strerror(int code);
 const char* fit_last_error(void);
 /* 128-byte RCCL unique id for a node-sharded group (rank 0 creates, everyone passes it). */
 int fit_nccl_unique_id(void* out128);
+/* Watchdog of the persistent engines: every device-side wait gives up after `us` microseconds
+ * (default 10 s, or FIT_WATCHDOG_MS); us <= 0 restores the default.  A trip fails the call with
+ * FIT_E_HIP, fit_last_error() names the wait (site, component, round, tile, ring indices, how long
+ * it waited), and the context stays usable: fit_place restores the node table it started from;
+ * fit_place_tl drops the timeline (FIT_E_STATE until fit_load_timeline).  Persistent launches of
+ * all contexts on one GPU — in every process — run one at a time (a per-device lock file in
+ * FIT_LOCK_DIR, default /tmp; fit_stats.ms_arb_wait). */
+int fit_set_watchdog_us(fit_ctx* ctx, int64_t us);
 
 /* Node table: one row per Slurm node, in Client.Nodes output order (pkg/slurm-agent/slurm.go:
  * 343-364); the row index is the node id placements refer to.  free = total - alloc (the

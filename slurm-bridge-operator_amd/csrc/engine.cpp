@@ -4,8 +4,13 @@
 // Boundary: include/fitgpu.h.  Everything here is plain C++ over the HIP runtime; the compute
 // is in fit_kernels.hip.  There is no CPU placement path: without a gfx950 device fit_create
 // fails with FIT_E_NODEV.
+#include <errno.h>
+#include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -13,6 +18,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -46,6 +53,7 @@ hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, 
 size_t engine_lds_bytes(int32_t max_component_nodes);
 size_t engine_ctl_bytes();
 size_t engine_ctl_error_offset();
+size_t engine_ctl_trip_offset();
 size_t engine_ring_bytes();
 size_t engine_ring_tasks();
 int engine_blocks_per_cu(size_t lds);
@@ -54,7 +62,7 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
                          const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
-                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk);
+                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk, unsigned wd);
 // time-windowed backfill (fit_timeline.hip)
 hipError_t launch_build_tl(hipStream_t st, const int32_t* cpu, const int32_t* mem,
                            const int32_t* gpu, const int32_t* av, const uint32_t* mask,
@@ -85,7 +93,7 @@ hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, v
                             const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
                             const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
                             int32_t slot_min, int32_t R, int64_t* wbusy, int mode,
-                            unsigned* resident);
+                            unsigned* resident, unsigned wd);
 hipError_t launch_expand_tl(hipStream_t st, const int32_t* perm, const Seg* slab,
                             const TlHdr* hdr, int32_t nn, int32_t H, int32_t* oc, int32_t* om,
                             int32_t* og);
@@ -181,6 +189,76 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// ---- per-device arbitration of persistent launches (round 5) --------------------------------
+// A persistent launch (k_engine / k_engine_tl) needs its committer blocks resident while its scan
+// workers spin on the task ring.  Alone on the GPU every block of its grid is resident (the grid
+// is sized by occupancy).  Two side by side are not: the dispatcher hands each grid's blocks to
+// the 8 XCDs in block order, so launch A's committer on XCD k can queue behind launch B's blocks
+// while A's workers fill the other XCDs waiting for it — and B's committer waits behind A's
+// workers (GPUTEST_r04: the watchdog tripped with three contexts on one GPU).  One virtual kubelet
+// per partition (pkg/configurator/configurator.go:151-171) means several contexts per GPU, in
+// several processes, so every persistent launch on a device is serialised: a process-wide mutex
+// per device, then an exclusive flock on <FIT_LOCK_DIR or /tmp>/fitgpu-<PCI bus id>.lock for the
+// other processes (flock: released by the kernel if the holder dies).  Held from the launch to
+// the stream synchronisation that ends it.  The host-driven rounds (k_scan / k_commit, no
+// cross-block waits) need no arbitration.
+struct DevArb {
+    std::mutex mu;
+    int fd = -1;
+    std::string path;
+};
+
+DevArb* dev_arb(int device, std::string& err) {
+    static std::mutex m;
+    static std::map<int, DevArb*> tab;
+    std::lock_guard<std::mutex> g(m);
+    DevArb*& a = tab[device];
+    if (!a) a = new DevArb();  // one per device for the process lifetime
+    if (a->fd < 0) {
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) snprintf(bus, sizeof bus, "dev%d", device);
+        for (char* q = bus; *q; ++q)
+            if (*q == ':' || *q == '/') *q = '_';
+        const char* dir = getenv("FIT_LOCK_DIR");
+        a->path = std::string(dir && *dir ? dir : "/tmp") + "/fitgpu-" + bus + ".lock";
+        const mode_t um = umask(0);
+        a->fd = open(a->path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+        umask(um);
+        if (a->fd < 0) {
+            err = a->path + ": " + strerror(errno);
+            return nullptr;
+        }
+    }
+    return a;
+}
+
+struct ArbGuard {
+    DevArb* a = nullptr;
+    double waited_ms = 0;
+    int take(int device) {
+        const double t0 = now_ms();
+        std::string err;
+        DevArb* d = dev_arb(device, err);
+        if (!d) return fail(FIT_E_STATE, "device lock %s (set FIT_LOCK_DIR to a writable directory)", err.c_str());
+        d->mu.lock();
+        int r;
+        do r = flock(d->fd, LOCK_EX);
+        while (r != 0 && errno == EINTR);
+        if (r != 0) {
+            d->mu.unlock();
+            return fail(FIT_E_STATE, "flock %s: %s", d->path.c_str(), strerror(errno));
+        }
+        a = d;
+        waited_ms = now_ms() - t0;
+        return 0;
+    }
+    ~ArbGuard() {
+        if (!a) return;
+        (void)flock(a->fd, LOCK_UN);
+        a->mu.unlock();
+    }
+};
+
 }  // namespace
 
 struct fit_ctx {
@@ -195,6 +273,10 @@ struct fit_ctx {
     bool force_coll = false;         // FIT_FLAG_COLLECTIVES: sharded path + exchange at world 1
     bool collective() const { return world > 1 || force_coll; }
     bool persistent = true;          // one-launch work-queue engine (FIT_ENGINE=rounds: host loop)
+    // placements of at most this many jobs (after the partition-limit prefilter) run the
+    // host-driven rounds instead of a whole-chip persistent grid: an admission batch of a few
+    // hundred pods is one or two rounds of a few tiles (FIT_SMALL_BATCH)
+    int32_t small_batch = 2048;
     int cus = 256;
     DBuf<uint8_t> ectl, ering;
     DBuf<CompState> ecs;
@@ -204,6 +286,9 @@ struct fit_ctx {
     HBuf<CompOut> h_eco;
     HBuf<int64_t> h_ebusy;
     HBuf<uint32_t> h_err;
+    HBuf<TripRec> h_trip;
+    DBuf<NodeRec> rec_bak;           // node rows before a persistent launch (restored on a trip)
+    unsigned wd_ticks = 1000000000u; // watchdog: realtime ticks (10 ns) a wait may last (10 s)
     HBuf<uint64_t> h_count;
     hipStream_t st = nullptr;
     hipEvent_t ev[6] = {};
@@ -292,6 +377,8 @@ struct fit_ctx {
         h_eco.release();
         h_ebusy.release();
         h_err.release();
+        h_trip.release();
+        rec_bak.release();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (ev_join) (void)hipEventDestroy(ev_join);
@@ -411,6 +498,31 @@ int xchg(fit_ctx* c, int op, void* dbuf, int64_t count) {
 }
 
 // ------------------------------------------------------------- persistent engine path
+const char* trip_site_name(unsigned s) {
+    switch (s) {
+        case TRIP_WORKER_RING: return "scan worker waiting for a task";
+        case TRIP_ROUND_START: return "committer waiting for the round before last";
+        case TRIP_HELPER_TILE: return "commit helper waiting for a scan tile";
+        case TRIP_HELPER_SNAP: return "commit helper waiting for the decider";
+        case TRIP_DECIDER_REC: return "decider waiting for a helper record";
+        case TRIP_SINGLE_TILE: return "single-wave commit waiting for a scan tile";
+        case TRIP_NO_PROGRESS: return "round resolved no job";
+        case TRIP_NO_KERNEL: return "no scan kernel for the key count";
+        default: return "unknown";
+    }
+}
+
+// The launch's error word and first trip record (read back with it): FIT_E_HIP with every field.
+int trip_error(fit_ctx* c, const char* engine) {
+    const TripRec& t = *c->h_trip.p;
+    return fail(FIT_E_HIP,
+                "%s watchdog tripped (code %u): site %u (%s), component %u, round %u, arg %u, "
+                "block %u, q_head %u, q_tail %u, pubt %u, tdone %u / need %u, waited %.3f ms, "
+                "%.3f ms into the launch (deadline %.3f ms)",
+                engine, c->h_err.p[0], t.site, trip_site_name(t.site), t.comp, t.round, t.arg,
+                t.block, t.q_head, t.q_tail, t.pubt, t.tdone, t.need, t.waited / 1e5, t.when / 1e5,
+                c->wd_ticks / 1e5);
+}
 // All rounds of all owned components in one launch (fit_persistent.hip).
 int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector<char>& owned,
                    const int32_t* cpu, const int32_t* mem, const int32_t* gpu, const int32_t* wall,
@@ -493,23 +605,42 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     // the serial commit chain (measured: 2/CU → commit +3%, no scan gain).
     int workers = std::max(8, std::max(1, per_cu - 1) * c->cus - nc);
     if (const char* e = getenv("FIT_WORKERS")) workers = std::max(1, atoi(e));
-    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers)) return FIT_E_OOM;
+    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers) || c->h_trip.ensure(1) ||
+        c->rec_bak.ensure(std::max(c->nn, 1)))
+        return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
     // every bound KEY_INF: a round resets only the bounds its buffer set's last round used
     HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * 2 * nc * wcap, st));
-    HIP_TRY(hipEventRecord(c->ev[0], st));
-    HIP_TRY(launch_engine(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
-                          c->plan.p, nc, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
-                          c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p, c->jpk.p));
-    HIP_TRY(hipEventRecord(c->ev[1], st));
-    HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + engine_ctl_error_offset(), 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (c->h_err.p[0]) return fail(FIT_E_HIP, "placement engine watchdog tripped (code %u)", c->h_err.p[0]);
+    // the node rows as they were: a trip leaves them partly committed, and the context must stay
+    // usable after FIT_E_HIP (restored below)
+    HIP_TRY(hipMemcpyAsync(c->rec_bak.p, c->rec.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
+    {
+        ArbGuard arb;  // one persistent launch per device at a time (see DevArb)
+        int rc = arb.take(c->device);
+        if (rc) return rc;
+        S.ms_arb_wait = arb.waited_ms;
+        HIP_TRY(hipEventRecord(c->ev[0], st));
+        HIP_TRY(launch_engine(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
+                              c->plan.p, nc, c->rec.p, c->jl.p, cpu, mem, gpu, wall, part, nk,
+                              c->cand.p, c->bnd.p, c->wjob.p, out, kmax, c->ebusy.p, c->jpk.p,
+                              c->wd_ticks));
+        HIP_TRY(hipEventRecord(c->ev[1], st));
+        HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * nc, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + engine_ctl_error_offset(), 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_trip.p, c->ectl.p + engine_ctl_trip_offset(), sizeof(TripRec),
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (c->h_err.p[0]) {
+        const int rc = trip_error(c, "placement engine");
+        HIP_TRY(hipMemcpyAsync(c->rec.p, c->rec_bak.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return rc;
+    }
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device += ms;
@@ -608,8 +739,10 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     const int srank = node_sharded ? c->rank : 0;
 
     // 3. speculative rounds: one persistent launch, or the host-driven loop (node sharding
-    // exchanges candidates over RCCL every round, so it keeps the host loop)
-    if (c->persistent && !node_sharded) {
+    // exchanges candidates over RCCL every round, so it keeps the host loop; a small batch is
+    // cheaper as a round or two of k_scan / k_commit than as a whole-chip persistent grid)
+    const bool small = J - S.rejected <= c->small_batch;
+    if (c->persistent && !node_sharded && !small) {
         int rc = run_persistent(c, jb, owned, cpu, mem, gpu, wall, part, nk, out, kmax, S);
         if (rc) return rc;
         S.engine = 1;
@@ -813,19 +946,26 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
             hipHostMalloc(&c->resident, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return fail(FIT_E_HIP, "split launch: stream / event / mapped flag");
     }
-    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers)) return FIT_E_OOM;
+    if (c->ebusy.ensure(2 * workers) || c->h_ebusy.ensure(2 * workers) || c->h_trip.ensure(1))
+        return FIT_E_OOM;
     HIP_TRY(hipMemcpyAsync(c->ecs.p, c->h_ecs.p, sizeof(CompState) * nc, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->ectl.p, 0, engine_ctl_bytes(), st));
     HIP_TRY(hipMemsetAsync(c->ering.p, 0, engine_ring_bytes(), st));
     // every bound KEY_INF: a round resets only the bounds its buffer set's last round used
     HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * 2 * nc * wcap, st));
+    ArbGuard arb;  // one persistent launch per device at a time (see DevArb); to the sync below
+    {
+        int rc = arb.take(c->device);
+        if (rc) return rc;
+        S.ms_arb_wait = arb.waited_ms;
+    }
     HIP_TRY(hipEventRecord(c->ev[0], st));
     bool resident_late = false;
     if (!split) {
         HIP_TRY(launch_engine_tl(nc + workers, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
                                  c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
                                  part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
-                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 0, nullptr));
+                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 0, nullptr, c->wd_ticks));
     } else {
         __atomic_store_n(c->resident, 0u, __ATOMIC_RELEASE);
         unsigned* dres = nullptr;
@@ -833,7 +973,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         HIP_TRY(launch_engine_tl(nc, lds, st, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p, c->plan.p,
                                  nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall, part,
                                  c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs, c->tl_slots,
-                                 c->tl_slot_min, R, c->ebusy.p, 1, dres));
+                                 c->tl_slot_min, R, c->ebusy.p, 1, dres, c->wd_ticks));
         // the workers go in once every committer block holds its CU (a worker block on a CU
         // would leave a committer no room, and the committers' rounds wait for workers)
         const auto t0 = std::chrono::steady_clock::now();
@@ -847,7 +987,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         HIP_TRY(launch_engine_tl(workers, lds_w, c->st2, c->ectl.p, c->ering.p, c->ecs.p, c->eco.p,
                                  c->plan.p, nc, c->slab.p, c->tlhdr.p, c->jl.p, cpu, mem, gpu, wall,
                                  part, c->cand.p, c->bnd.p, c->wjob.p, c->perm.p, out, outs,
-                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 2, nullptr));
+                                 c->tl_slots, c->tl_slot_min, R, c->ebusy.p, 2, nullptr, c->wd_ticks));
         HIP_TRY(hipEventRecord(c->ev_join, c->st2));
         HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
     }
@@ -856,9 +996,19 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
     HIP_TRY(hipMemcpyAsync(c->h_ebusy.p, c->ebusy.p, sizeof(int64_t) * 2 * workers,
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_err.p, c->ectl.p + engine_ctl_error_offset(), 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_trip.p, c->ectl.p + engine_ctl_trip_offset(), sizeof(TripRec),
+                           hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (c->h_err.p[0]) return fail(FIT_E_HIP, "timeline engine watchdog tripped (code %u)", c->h_err.p[0]);
-    if (resident_late) return fail(FIT_E_HIP, "timeline engine: committer blocks not resident after 10 s");
+    // a trip leaves the run lists partly reserved: the timeline must be loaded again (a copy of
+    // the slab per placement would cost more than the rare reload); the node table is untouched
+    if (c->h_err.p[0]) {
+        c->have_tl = false;
+        return trip_error(c, "timeline engine");
+    }
+    if (resident_late) {
+        c->have_tl = false;
+        return fail(FIT_E_HIP, "timeline engine: committer blocks not resident after 10 s");
+    }
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device += ms;
@@ -908,7 +1058,7 @@ int place_tl_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem,
     const int shards = c->world, srank = c->rank;
     S.shard_mode = node_sharded ? FIT_SHARD_NODES : 0;
     S.components = C;
-    if (c->persistent && !node_sharded) {
+    if (c->persistent && !node_sharded && J - S.rejected > c->small_batch) {
         rc = run_persistent_tl(c, jb, cpu, mem, gpu, wall, part, out, outs, S);
         if (rc) return rc;
         S.unplaced = J - S.placed - S.rejected;
@@ -1110,7 +1260,15 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (!c) return fail(FIT_E_OOM, "context allocation");
     c->device = dev;
     c->cus = prop.multiProcessorCount;
-    if (const char* ev = getenv("FIT_ENGINE")) c->persistent = strcmp(ev, "rounds") != 0;
+    if (const char* ev = getenv("FIT_WATCHDOG_MS"))
+        c->wd_ticks = (unsigned)std::min<double>(4.29e9, std::max(1.0, atof(ev) * 1e5));
+    // FIT_ENGINE: "rounds" = host-driven rounds always, "persistent" = the persistent engine at
+    // every size; unset = persistent above small_batch jobs (FIT_SMALL_BATCH)
+    if (const char* ev = getenv("FIT_SMALL_BATCH")) c->small_batch = atoi(ev);
+    if (const char* ev = getenv("FIT_ENGINE")) {
+        c->persistent = strcmp(ev, "rounds") != 0;
+        if (strcmp(ev, "persistent") == 0) c->small_batch = -1;
+    }
     c->rank = o.rank;
     c->world = o.world;
     c->force_coll = (o.flags & FIT_FLAG_COLLECTIVES) != 0;
@@ -1153,6 +1311,19 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
         return rc;
     }
     *out_ctx = c;
+    return 0;
+}
+
+int fit_set_watchdog_us(fit_ctx* c, int64_t us) {
+    if (!c) return fail(FIT_E_INVAL, "null ctx");
+    if (us <= 0) {
+        c->wd_ticks = 1000000000u;
+        if (const char* ev = getenv("FIT_WATCHDOG_MS"))
+            c->wd_ticks = (unsigned)std::min<double>(4.29e9, std::max(1.0, atof(ev) * 1e5));
+        return 0;
+    }
+    // 100 realtime ticks per microsecond; the ticks are a 32-bit kernel argument (<= 42.9 s)
+    c->wd_ticks = (unsigned)std::min<int64_t>(us * 100, 4290000000ll);
     return 0;
 }
 

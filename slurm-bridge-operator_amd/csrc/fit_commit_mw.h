@@ -62,7 +62,6 @@ constexpr int MW_H = MW_WAVES - 1;  // helpers: waves 1..7
 static_assert(MW_M == 8, "the decider holds one item per lane of its 8-lane ring group");
 static_assert(MW_R >= MW_M, "record slot reuse relies on the lag bound");
 
-constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 #ifndef MW_HSLEEP
 #define MW_HSLEEP 1  // helper back-off per missing decided job, in units of 64 cycles (12 before the
                       // 4-entry helpers: C3 k_engine 32.2 -> 31.2 ms at 0-2)
@@ -100,10 +99,12 @@ struct alignas(16) MwRec {
 struct alignas(16) MwShared {
     uint64_t dn;       // {decided (low 32), nu (high 32)}: the helpers' snapshot, release-stored
     uint32_t halt;     // decider stopped
-    uint32_t fail;     // helper / decider watchdog
+    uint32_t fail;     // helper / decider watchdog: the TripSite of the first wait that gave up
     int32_t res[4];    // CommitResult of the window
     uint32_t pubt;     // job tiles of the window published to the task ring (MwTiles::ring)
-    uint32_t pad[7];
+    uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer)
+    uint32_t trip_arg; // the failed wait's tile / record
+    uint32_t pad[5];
     MwRec rec[MW_R];
     MwRow rows[UCAP];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
@@ -143,6 +144,19 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+
+// A commit wait gave up (uniform call; helper or decider): the block's first failure names its
+// TripSite and argument in `fail` / `trip_arg`; `fail` stops every wave of the block and the
+// committer turns it into the launch's trip record (fit_engine_ctl.h trip_record).
+__device__ __forceinline__ void commit_fail(uint32_t* fail, uint32_t* trip_arg, uint32_t site,
+                                            uint32_t arg) {
+    if ((threadIdx.x & 63u) == 0u) {
+        uint32_t none = 0u;
+        if (__hip_atomic_compare_exchange_strong(fail, &none, site, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+            lds_st(trip_arg, arg);
+    }
+}
 
 // Tile readiness: the window's scan tiles complete while the window is being
 // committed; a helper waits for the (job tile)'s per-tile counter to reach nslice before reading
@@ -413,13 +427,18 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
     if (tile < ready) return true;
     if (T.ring && (unsigned)tile + ENGINE_AHEAD > lds_ld(&S->pubt))
         mw_publish(T, S, min((unsigned)tile + ENGINE_AHEAD, T.ntj));
+    const unsigned long long t0 = realtime();
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
             T.need)
             break;
         if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if (sp > MW_SPIN_LIMIT) {
-            lds_st(&S->fail, 1u);
+        if ((sp & 63u) == 63u && T.ctl && ld_agent(&T.ctl->error)) {  // another block tripped
+            commit_fail(&S->fail, &S->trip_arg, TRIP_PEER, (uint32_t)tile);
+            return false;
+        }
+        if (wd_over(sp, t0, lds_ld(&S->wd))) {
+            commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -610,13 +629,15 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
            record slot i & 7's previous one) */                                                \
         uint64_t dn_;                                                                          \
         MW_CLK(hw0_);                                                                          \
+        unsigned long long st0_ = 0ull;                                                        \
         for (unsigned sp_ = 0;; ++sp_) {                                                       \
             dn_ = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
             const int lag_ = i - (MW_SNAP - 1) - rfl((int32_t)(uint32_t)dn_);                  \
             if (lag_ <= 0) break;                                                              \
             if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
-            if (sp_ > MW_SPIN_LIMIT) {                                                         \
-                lds_st(&S->fail, 1u);                                                          \
+            if (sp_ == 0u) st0_ = realtime();                                                  \
+            else if (wd_over(sp_, st0_, lds_ld(&S->wd))) {                                     \
+                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_SNAP, (uint32_t)i);            \
                 goto hdone;                                                                    \
             }                                                                                  \
             /* the decider needs ~1k cycles a job: sleep about that long per missing job      \
@@ -954,11 +975,12 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     if (__builtin_expect(!D.exit && (rec_missing || d.stopB || d.full), 0)) {  // the one branch
         if (rec_missing) {  // record t not complete when read: wait for it, read it again
             MW_CLK(c0);
+            const unsigned long long w0 = realtime();
             for (unsigned sp = 0;; ++sp) {
                 flag = lds_ld(&S->rec[t & (MW_R - 1)].h.ready);
                 if (flag == (uint32_t)t + 1u) break;
-                if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                    lds_st(&S->fail, 1u);
+                if (lds_ld(&S->fail) || wd_over(sp, w0, lds_ld(&S->wd))) {
+                    commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, (uint32_t)t);
                     D.stop = 3;
                     D.exit = true;
                     break;
@@ -1070,14 +1092,15 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MwRecRegs ra, rb;
     uint32_t flag = 0;
     if (P.w > 0) {
+        const unsigned long long w0 = realtime();
         for (unsigned sp = 0;; ++sp) {
             flag = lds_ld(&S->rec[0].h.ready);
 #ifdef MW_DECIDER_BENCH
             break;
 #endif
             if (flag == 1u) break;
-            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                lds_st(&S->fail, 1u);
+            if (lds_ld(&S->fail) || wd_over(sp, w0, lds_ld(&S->wd))) {
+                commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, 0u);
                 D.stop = 3;
                 D.exit = true;
                 break;

@@ -70,10 +70,12 @@ struct alignas(16) TmSlot {  // one dirty slot, current (written by the decider)
 struct alignas(16) TmShared {
     uint64_t dn;       // {decided (low 32), nu (high 32)}: the helpers' snapshot, release-stored
     uint32_t halt;     // decider stopped
-    uint32_t fail;     // helper / decider watchdog
+    uint32_t fail;     // helper / decider watchdog: the TripSite of the first wait that gave up
     int32_t res[4];    // CommitResult of the window
     uint32_t pubt;     // job tiles of the window published to the task ring (just in time)
-    uint32_t pad[7];
+    uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer)
+    uint32_t trip_arg; // the failed wait's tile / record
+    uint32_t pad[5];
     TmRec rec[TM_R];
     Seg stage[TM_R][64];     // the run list of each record's first clean item
     TmSlot slot[TL_UCAP];
@@ -133,12 +135,17 @@ __device__ __forceinline__ bool tm_tile_ready(const MwTiles& T, int tt, int& rea
         tm_publish(T, S, min((unsigned)tile + TL_AHEAD, T.ntj));
     const unsigned* tdone = T.tdone;
     const unsigned need = T.need;
+    const unsigned long long t0 = realtime();
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
             break;
         if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if (sp > MW_SPIN_LIMIT) {
-            lds_st(&S->fail, 1u);
+        if ((sp & 63u) == 63u && T.ctl && ld_agent(&T.ctl->error)) {  // another block tripped
+            commit_fail(&S->fail, &S->trip_arg, TRIP_PEER, (uint32_t)tile);
+            return false;
+        }
+        if (wd_over(sp, t0, lds_ld(&S->wd))) {
+            commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -324,13 +331,15 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         // snapshot: the decider has resolved at least t - (TM_M - 1) jobs (so it has read record
         // slot t & 7's previous job)
         uint64_t dn;
+        unsigned long long st0 = 0ull;
         for (unsigned sp = 0;; ++sp) {
             dn = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const int lag = t - (TM_M - 1) - rfl((int32_t)(uint32_t)dn);
             if (lag <= 0) break;
             if ((sp & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) return;
-            if (sp > MW_SPIN_LIMIT) {
-                lds_st(&S->fail, 1u);
+            if (sp == 0u) st0 = realtime();
+            else if (wd_over(sp, st0, lds_ld(&S->wd))) {
+                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_SNAP, (uint32_t)t);
                 return;
             }
             for (int s = min(lag, 8); s > 0; --s) __builtin_amdgcn_s_sleep(2);
@@ -645,11 +654,12 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         if (__builtin_expect(!D.exit && (rec_missing || need_walk || D.gm != 0ull), 0)) {
             if (rec_missing) {  // record t not complete when read: wait for it, read it again
                 TM_CLK(w0);
+                const unsigned long long rw0 = realtime();
                 for (unsigned sp = 0;; ++sp) {
                     flag = lds_ld(&S->rec[t & (TM_R - 1)].h.ready);
                     if (flag == (uint32_t)t + 1u) break;
-                    if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                        lds_st(&S->fail, 1u);
+                    if (lds_ld(&S->fail) || wd_over(sp, rw0, lds_ld(&S->wd))) {
+                        commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, (uint32_t)t);
                         D.stop = 3;
                         D.exit = true;
                         break;
@@ -898,11 +908,12 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     const unsigned long long k0 = __builtin_amdgcn_s_memtime();
 #endif
     if (P.w > 0) {
+        const unsigned long long rw0 = realtime();
         for (unsigned sp = 0;; ++sp) {
             flag = lds_ld(&S->rec[0].h.ready);
             if (flag == 1u) break;
-            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                lds_st(&S->fail, 1u);
+            if (lds_ld(&S->fail) || wd_over(sp, rw0, lds_ld(&S->wd))) {
+                commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, 0u);
                 D.stop = 3;
                 D.exit = true;
                 break;

@@ -141,4 +141,25 @@ struct CommitResult {
     int32_t placed;
 };
 
+// Persistent engines' watchdog trip record (fit_engine_ctl.h; read back by engine.cpp).
+enum TripSite : unsigned {
+    TRIP_NONE = 0,
+    TRIP_WORKER_RING = 1,   // scan worker: its claimed ring slot got no task (arg = ring index)
+    TRIP_ROUND_START = 2,   // committer: tiles of the round before last not done (arg = target)
+    TRIP_HELPER_TILE = 3,   // commit helper: a job tile's scan not done (arg = tile)
+    TRIP_HELPER_SNAP = 4,   // commit helper: the decider did not advance (arg = record)
+    TRIP_DECIDER_REC = 5,   // decider: a helper record not ready (arg = record)
+    TRIP_SINGLE_TILE = 6,   // single-wave commit: a job tile's scan not done (arg = tile)
+    TRIP_NO_PROGRESS = 7,   // a round resolved no job
+    TRIP_NO_KERNEL = 8,     // no scan kernel for the plan's key count
+    TRIP_PEER = 9,          // drained after another block's trip
+};
+struct TripRec {  // the launch's first trip (claim 0 -> 1); plain stores, read after the kernel
+    unsigned claim, site, comp, round;
+    unsigned arg, q_head, q_tail, pubt;
+    unsigned tdone, need, block, pad;
+    unsigned long long waited;  // realtime ticks (10 ns) the wait lasted
+    unsigned long long when;    // realtime at the trip, minus the launch's start stamp
+};
+
 }  // namespace fitgpu

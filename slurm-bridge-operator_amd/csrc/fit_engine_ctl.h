@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "fit_device.h"
+
 namespace fitgpu {
 
 #ifndef FIT_QCAP_LOG2
@@ -11,8 +13,18 @@ namespace fitgpu {
 #endif
 constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
-constexpr unsigned SPIN_LIMIT = 1u << 25;
 constexpr unsigned long long TASK_EXIT = ~0ull;
+
+// ---- watchdog (round 5) ----------------------------------------------------------------------
+// Every wait of the persistent engines is bounded in TIME: `wd` ticks of the 100 MHz realtime
+// counter since the wait began (a kernel argument; fit_set_watchdog_us, default 10 s).  A spin
+// count cannot tell a long legitimate wait (another tenant's kernel holding the CUs) from a hang.
+// The first trip of a launch records where it happened (TripRec); fit_last_error reports it.
+__device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
+// checked every 64 spins: the clock read is an SMEM round trip
+__device__ __forceinline__ bool wd_over(unsigned spins, unsigned long long t0, unsigned wd) {
+    return (spins & 63u) == 63u && realtime() - t0 > (unsigned long long)wd;
+}
 
 struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned q_tail;   // tiles reserved by committers
@@ -39,10 +51,46 @@ struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     // component and pair, the halves finished (the second merges both lists)
     unsigned tpair[2][32][32];
     unsigned long long pub[32];        // FIT_STAMPS: realtime of each component's last publish
+    unsigned long long t_start;        // realtime when the first block started (min, TripRec::when)
+    TripRec trip;
 };
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Record a trip (one lane): the first trip of the launch claims ctl->trip and describes itself;
+// every trip ORs its error bit, which drains all blocks.
+static __device__ __noinline__ void trip_record(EngineCtl* ctl, unsigned bit, unsigned site, unsigned comp,
+                                               unsigned round, unsigned arg, unsigned pubt, unsigned tdone,
+                                               unsigned need, unsigned long long t0) {
+    if (site != TRIP_PEER &&
+        __hip_atomic_fetch_or(&ctl->trip.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        const unsigned long long now = realtime();
+        TripRec& r = ctl->trip;
+        r.site = site;
+        r.comp = comp;
+        r.round = round;
+        r.arg = arg;
+        r.q_head = ld_agent(&ctl->q_head);
+        r.q_tail = ld_agent(&ctl->q_tail);
+        r.pubt = pubt;
+        r.tdone = tdone;
+        r.need = need;
+        r.block = blockIdx.x;
+        r.waited = now - t0;
+        const unsigned long long ts = __hip_atomic_load(&ctl->t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.when = ts && now > ts ? now - ts : 0ull;
+    }
+    __hip_atomic_fetch_or(&ctl->error, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the launch's start stamp (the first block to arrive; one lane per block)
+__device__ __forceinline__ void stamp_start(EngineCtl* ctl) {
+    const unsigned long long now = realtime();
+    unsigned long long none = 0ull;
+    if (__hip_atomic_load(&ctl->t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull)
+        __hip_atomic_compare_exchange_strong(&ctl->t_start, &none, now, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Task word: {epoch:32 | skip:1 | round:12 | tile:7 | slice:6 | component:6}.  done[c][1] holds
@@ -125,13 +173,21 @@ __device__ __forceinline__ void release_agent() {
 }
 
 // Spin (wave 0 of a committer) until component c has completed `target` scan tiles of the
-// rounds with parity p.
-__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, int p, unsigned target) {
-    for (unsigned spins = 0; ld_agent(&ctl->done[c][2 + p]) < target;) {
-        if (++spins > SPIN_LIMIT || ld_agent(&ctl->error)) return false;
+// rounds with parity p.  false: another block tripped, or this wait outlasted `wd` (recorded).
+__device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, int p, unsigned target,
+                                           unsigned wd, unsigned round) {
+    const unsigned long long t0 = realtime();
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned d = ld_agent(&ctl->done[c][2 + p]);
+        if (d >= target) return true;
+        if (ld_agent(&ctl->error)) return false;
+        if (wd_over(spins, t0, wd)) {
+            if ((threadIdx.x & 63u) == 0u)
+                trip_record(ctl, 1u, TRIP_ROUND_START, (unsigned)c, round, target, 0u, d, target, t0);
+            return false;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
-    return true;
 }
 
 }  // namespace fitgpu

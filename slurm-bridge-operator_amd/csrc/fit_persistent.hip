@@ -63,9 +63,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk,
     uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd, JobRec* __restrict__ wjob,
     int32_t* __restrict__ out, int kmax, int64_t* __restrict__ wbusy,
-    const int32_t* __restrict__ jpk) {
+    const int32_t* __restrict__ jpk, unsigned wd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) stamp_start(ctl);
 
     if ((int)blockIdx.x < ncomp) {
         // ================================================================== committer
@@ -76,6 +77,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
         const int c = blockIdx.x;
         const CompState S = cs[c];
         MwShared* M = reinterpret_cast<MwShared*>(smem);
+        if (threadIdx.x == 0) M->wd = wd;  // the commit waits' deadline (fit_commit_mw.h)
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity
         // job tiles published by the last round of each parity: only their bounds can differ from
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 // the tiles of the round before last (this round's buffer set; also those past its
                 // stop) must all be complete before their buffers and counters are reused; the
                 // previous round's may still be in flight, in the other set
-                bool fail = !wait_tiles(ctl, c, par, target[par]);
+                bool fail = !wait_tiles(ctl, c, par, target[par], wd, rnd);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 // written through (sc1), like the tile counters: the helpers that publish tiles
                 // just in time need no release of their own (R1: stored, drained, then the
@@ -164,8 +166,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 }
                 if (npub == ntj) target[par] += ntiles;  // else: after the commit (M->pubt)
-                if (multi && !fail) fail = !wait_tiles(ctl, c, par, target[par]);
-                if (fail && lane == 0) atomicOr(&ctl->error, 1u);
+                if (multi && !fail) fail = !wait_tiles(ctl, c, par, target[par], wd, rnd);
                 acquire_agent();  // node rows written by this block: CU-wide view for all waves
                 if (lane == 0) s_fail = fail;
                 {
@@ -207,12 +208,20 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             }
             if (wave == 0) used[par] = M->pubt;  // stable after the commit's closing barrier
             if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
-            if (R.stop == 3) {  // commit watchdog
-                if (threadIdx.x == 0) atomicOr(&ctl->error, 2u);
+            if (R.stop == 3) {  // a commit wait gave up: M->fail names it (TRIP_PEER: drained)
+                if (threadIdx.x == 0) {
+                    const unsigned site = M->fail ? M->fail : (unsigned)TRIP_SINGLE_TILE;
+                    const unsigned tl = site == TRIP_HELPER_TILE ? M->trip_arg : 0u;
+                    trip_record(ctl, site == TRIP_PEER ? 0u : 2u, site, (unsigned)c, rnd, M->trip_arg,
+                                M->pubt, ld_agent(&ctl->tdone[par][c][tl & (ENGINE_TILES - 1)]),
+                                (unsigned)S.nslice, (unsigned long long)t1);
+                }
                 break;
             }
             if (R.done == 0) {  // the next round would rescan the same state: never progresses
-                if (threadIdx.x == 0) atomicOr(&ctl->error, 4u);
+                if (threadIdx.x == 0)
+                    trip_record(ctl, 4u, TRIP_NO_PROGRESS, (unsigned)c, rnd, (unsigned)cursor, M->pubt,
+                                0u, 0u, (unsigned long long)t1);
                 break;
             }
             prev_multi = multi;
@@ -253,6 +262,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                                                         __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
             unsigned long long task = TASK_EXIT;
+            const unsigned long long w0 = realtime();
             for (unsigned spins = 0;; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
@@ -262,8 +272,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     break;
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (spins > SPIN_LIMIT) {
-                    atomicOr(&ctl->error, 1u);
+                if (wd_over(spins, w0, wd)) {
+                    trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
+                                (unsigned)ncomp, w0);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -359,7 +370,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 SCAN_K(2)
 #undef SCAN_K
                 default:  // no scan kernel for this key count: trip the watchdog, never guess
-                    if (threadIdx.x == 0) atomicOr(&ctl->error, 8u);
+                    if (threadIdx.x == 0)
+                        trip_record(ctl, 8u, TRIP_NO_KERNEL, (unsigned)c, task_round(task), (unsigned)P.ks,
+                                    0u, 0u, 0u, realtime());
                     break;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
@@ -399,6 +412,7 @@ size_t engine_lds_bytes(int32_t max_component_nodes) {
 
 size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
 size_t engine_ctl_error_offset() { return offsetof(EngineCtl, error); }
+size_t engine_ctl_trip_offset() { return offsetof(EngineCtl, trip); }
 size_t engine_ring_bytes() { return sizeof(unsigned long long) * QCAP; }
 size_t engine_ring_tasks() { return QCAP; }  // task-ring entries
 
@@ -415,12 +429,12 @@ hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void
                          const int32_t* jl, const int32_t* jcpu, const int32_t* jmem,
                          const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
                          const uint16_t* jk, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
-                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk) {
+                         int32_t* out, int kmax, int64_t* wbusy, const int32_t* jpk, unsigned wd) {
     hipLaunchKernelGGL(k_engine, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,
                        static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),
                        static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,
                        rec, jl, jcpu, jmem, jgpu, jwall, jpart, jk, cand, bnd, wjob, out, kmax,
-                       wbusy, jpk);
+                       wbusy, jpk, wd);
     return hipGetLastError();
 }
 

@@ -690,9 +690,10 @@ __device__ __forceinline__ CommitResult commit_tl_window(
         if (!tdone) return true;
         const int tile = tt / SCAN_JOBS;
         if (tile < ready) return true;
+        const unsigned long long t0 = realtime();
         for (unsigned sp = 0;; ++sp) {
             if (__hip_atomic_load(tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-            if (sp > SPIN_LIMIT) return false;
+            if (wd_over(sp, t0, 1000000000u)) return false;  // 10 s
             __builtin_amdgcn_s_sleep(1);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1033,9 +1034,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     const uint16_t* __restrict__ jpart, uint64_t* __restrict__ cand, uint64_t* __restrict__ bnd,
     JobRec* __restrict__ wjob, const int32_t* __restrict__ perm, int32_t* __restrict__ out,
     int32_t* __restrict__ outs, int32_t H, int32_t slot_min, int32_t R,
-    int64_t* __restrict__ wbusy, unsigned* __restrict__ resident) {
+    int64_t* __restrict__ wbusy, unsigned* __restrict__ resident, unsigned wd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) stamp_start(ctl);
 
     if (MODE == 1 || (MODE == 0 && (int)blockIdx.x < ncomp)) {
         if (MODE == 1 && threadIdx.x == 0)
@@ -1047,6 +1049,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int c = blockIdx.x;
         const CompState S = cs[c];
+        if (threadIdx.x == 0) reinterpret_cast<TmShared*>(smem)->wd = wd;  // commit waits' deadline
         int32_t cursor = S.jstart, win = S.wmin;
         unsigned target[2] = {0u, 0u};  // tiles published by the rounds of each parity (fit_engine_ctl.h)
         unsigned used[2] = {0u, 0u};    // job tiles whose bounds the last round of each parity reset
@@ -1079,7 +1082,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             if (wave == 0) {
                 // the tiles of the window before last (this round's buffer set; also those past
                 // its stop) must all be complete before their buffers and counters are reused
-                bool f = !wait_tiles(ctl, c, par, target[par]);
+                bool f = !wait_tiles(ctl, c, par, target[par], wd, rnd);
                 const unsigned ntj = (unsigned)((w + SCAN_JOBS - 1) / SCAN_JOBS);
                 store_through(&plans[2 * c + par], P);  // as k_engine's (fit_persistent.hip)
                 const int nres = min((int)used[par] * SCAN_JOBS, S.wmax);  // within the slot region
@@ -1109,7 +1112,6 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 }
                 if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
-                if (f && lane == 0) atomicOr(&ctl->error, 1u);
                 acquire_agent();  // run lists written back by this block: CU-wide fresh view
                 if (lane == 0) s_fail = f;
                 fail = f;
@@ -1133,12 +1135,22 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 used[par] = reinterpret_cast<TmShared*>(smem)->pubt;
             }
             if (threadIdx.x == 0) engine_round_finished(ctl, c, rnd);
-            if (r.stop == 3) {
-                fail = true;
+            if (r.stop == 3) {  // a commit wait gave up: TmShared::fail names it (TRIP_PEER: drained)
+                if (threadIdx.x == 0) {
+                    const TmShared* M = reinterpret_cast<const TmShared*>(smem);
+                    const unsigned site = M->fail ? M->fail : (unsigned)TRIP_HELPER_TILE;
+                    const unsigned tl = site == TRIP_HELPER_TILE ? M->trip_arg : 0u;
+                    trip_record(ctl, site == TRIP_PEER ? 0u : 2u, site, (unsigned)c, rnd, M->trip_arg,
+                                M->pubt, ld_agent(&ctl->tdone[par][c][tl & (ENGINE_TILES - 1)]),
+                                (unsigned)S.nslice, (unsigned long long)t1);
+                }
                 break;
             }
             if (r.done == 0) {  // the next round would rescan the same state: never progresses
-                if (threadIdx.x == 0) atomicOr(&ctl->error, 4u);
+                if (threadIdx.x == 0)
+                    trip_record(ctl, 4u, TRIP_NO_PROGRESS, (unsigned)c, rnd, (unsigned)cursor,
+                                reinterpret_cast<const TmShared*>(smem)->pubt, 0u, 0u,
+                                (unsigned long long)t1);
                 break;
             }
             const int64_t t2 = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -1154,7 +1166,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             win = max(S.wmin, min(S.wmax, nw));
         }
         if (wave != 0) return;
-        if (fail && lane == 0) atomicOr(&ctl->error, 1u);
+        (void)fail;  // every failure above recorded its own trip (or drained after another's)
         release_agent();  // last window's run lists / placements (kernel end also flushes)
         if (lane == 0) {
             co[c] = CompOut{evals, placed, cursor - S.jstart, rounds, sr, sd, tc, tw};
@@ -1179,6 +1191,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 held = true;
             }
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
+            const unsigned long long w0 = realtime();
             for (unsigned spins = 0;; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
@@ -1189,8 +1202,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     break;
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (spins > SPIN_LIMIT) {
-                    atomicOr(&ctl->error, 1u);
+                if (wd_over(spins, w0, wd)) {
+                    trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
+                                (unsigned)ncomp, w0);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -1403,13 +1417,13 @@ hipError_t launch_engine_tl(int blocks, size_t lds, hipStream_t st, void* ctl, v
                             const uint16_t* jpart, uint64_t* cand, uint64_t* bnd, JobRec* wjob,
                             const int32_t* perm, int32_t* out, int32_t* outs, int32_t H,
                             int32_t slot_min, int32_t R, int64_t* wbusy, int mode,
-                            unsigned* resident) {
+                            unsigned* resident, unsigned wd) {
 #define FIT_ENGINE_TL(M_)                                                                         \
     hipLaunchKernelGGL(k_engine_tl<M_>, dim3(blocks), dim3(SCAN_WAVES * 64), lds, st,          \
                        static_cast<EngineCtl*>(ctl), static_cast<unsigned long long*>(ring),     \
                        static_cast<const CompState*>(cs), static_cast<CompOut*>(co), plans, ncomp,\
                        slab, hdr, jl, jcpu, jmem, jgpu, jwall, jpart, cand, bnd, wjob, perm, out,  \
-                       outs, H, slot_min, R, wbusy, resident)
+                       outs, H, slot_min, R, wbusy, resident, wd)
     if (mode == 1) FIT_ENGINE_TL(1);
     else if (mode == 2) FIT_ENGINE_TL(2);
     else FIT_ENGINE_TL(0);

@@ -417,6 +417,11 @@ class Engine:
               "fit_load_nodes_device")
         self.n = n
 
+    def set_watchdog_us(self, us: int):
+        """Deadline of every device-side wait of the persistent engines (fit_set_watchdog_us);
+        us <= 0 restores the default (10 s)."""
+        check(lib().fit_set_watchdog_us(self._h, int(us)), "fit_set_watchdog_us")
+
     def load_partitions(self, parts):
         cols = [np.ascontiguousarray(a, np.int32) for a in (parts.max_time_min, parts.max_cpus_per_node,
                                                             parts.max_mem_per_node)]

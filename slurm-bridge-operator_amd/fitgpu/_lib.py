@@ -39,7 +39,7 @@ EXPORTS = [
     "fit_admitter_reservations", "fit_admitter_pending", "fit_admitter_destroy",
     "fit_array_tasks", "fit_pod_demand", "fit_script_with_nodelist", "fit_partition_limits",
     "fit_node_columns", "fit_node_names", "fit_admitter_load_table", "fit_admitter_generation",
-    "fit_admitter_script", "fit_set_max_array_size", "fit_release_events",
+    "fit_admitter_script", "fit_set_max_array_size", "fit_release_events", "fit_set_watchdog_us",
 ]
 
 
@@ -63,7 +63,8 @@ class FitStats(C.Structure):
                 ("stops_dirty", C.c_int64), ("ms_total", C.c_double), ("ms_scan", C.c_double),
                 ("ms_commit", C.c_double), ("ms_exchange", C.c_double), ("ms_device", C.c_double),
                 ("shard_mode", C.c_int32),
-                ("components", C.c_int32), ("engine", C.c_int32), ("reserved", C.c_int32)]
+                ("components", C.c_int32), ("engine", C.c_int32), ("reserved", C.c_int32),
+                ("ms_arb_wait", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -133,6 +134,7 @@ def lib() -> C.CDLL:
         L.fit_destroy.argtypes = [P]
         L.fit_destroy.restype = None
         L.fit_nccl_unique_id.argtypes = [P]
+        L.fit_set_watchdog_us.argtypes = [P, i64]
         for name in ("fit_load_nodes", "fit_load_nodes_device"):
             getattr(L, name).argtypes = [P, i32, P, P, P, P, P]
         L.fit_load_partitions.argtypes = [P, i32, P, P, P]

@@ -34,6 +34,27 @@ func (e *Error) Error() string {
 	return fmt.Sprintf("fitgpu: %s (%d): %s", C.GoString(C.fit_strerror(C.int(e.Code))), e.Code, e.Detail)
 }
 
+// EngineFailure reports whether err is the engine failing rather than a decision about a pod:
+// a HIP / RCCL runtime error (a watchdog trip included), an allocation failure, no device, or
+// a context out of state.  Callers fall back to the reference path on these (INTEGRATION.md).
+func EngineFailure(err error) bool {
+	var fe *Error
+	if !errors.As(err, &fe) {
+		return false
+	}
+	switch fe.Code {
+	case int(C.FIT_E_HIP), int(C.FIT_E_RCCL), int(C.FIT_E_OOM), int(C.FIT_E_NODEV), int(C.FIT_E_STATE):
+		return true
+	}
+	return false
+}
+
+// SetWatchdog bounds every device-side wait of the persistent engines (fit_set_watchdog_us);
+// us <= 0 restores the default (10 s).
+func (e *Engine) SetWatchdog(us int64) error {
+	return check(C.fit_set_watchdog_us(e.ctx, C.int64_t(us)))
+}
+
 func check(rc C.int) error {
 	if rc < 0 {
 		return &Error{Code: int(rc), Detail: C.GoString(C.fit_last_error())}

@@ -197,7 +197,8 @@ func (f *FitAdmission) release(tickets []int64) {
 
 // CreatePodWithFit is CreatePod (provider.go:35-60) with the engine's admission in front of
 // SubmitJob and its nodes in the submitted script; provider.go's CreatePod delegates to it when
-// s.fit != nil.
+// s.fit != nil and needReconcile(pod).  An engine failure (fitgpu.EngineFailure) falls back to the
+// reference submission: unpinned, no reservation, logged.
 func (s *SlurmVirtualKubeletProvider) CreatePodWithFit(ctx context.Context, pod *v1.Pod, f *FitAdmission) error {
 	if !needReconcile(pod) {
 		return s.CreatePod(ctx, pod)
@@ -207,7 +208,15 @@ func (s *SlurmVirtualKubeletProvider) CreatePodWithFit(ctx context.Context, pod 
 	}
 	script, tickets, err := f.admit(pod)
 	if err != nil {
-		return err
+		if !fitgpu.EngineFailure(err) {
+			return err // a decision (no room now, over the partition's limits) or a bad pod
+		}
+		// the engine failed (a HIP error, a watchdog trip, no device): the pod goes the reference
+		// way instead of being retried against an engine that cannot answer — submitted as
+		// CreatePod submits it (provider.go:35-60): its own script, unpinned, no reservation
+		klog.Errorf("fit: engine failure admitting pod %s/%s, submitting it without a fit check: %v",
+			pod.Namespace, pod.Name, err)
+		script, tickets = pod.Spec.Containers[0].Command[0], nil
 	}
 	submitRequest := s.newSubmitRequestForPod(pod)
 	submitRequest.Script = script

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.fit_abi_version() == 7
+    assert L.fit_abi_version() == 8
     assert L.fit_strerror(_lib.FIT_E_NODEV) == b"no usable gfx950 device"
 
 

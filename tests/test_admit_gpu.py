@@ -15,7 +15,7 @@ from fitgpu import FIT_UNPLACED, Admitter, Engine, FitError, synth
 from fitgpu import _lib
 from oracle import pyoracle as po
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.auto_engine]
 
 
 def _run_workers(adm, reqs, workers=10):

@@ -25,7 +25,7 @@ from fitgpu import FIT_REJECTED, FIT_UNPLACED, Admitter, Engine, FitError, synth
 from fitgpu import _lib
 from oracle import pyoracle as po
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.auto_engine]
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SCRIPT = "#!/bin/sh\n#SBATCH --nodes=1\nsrun hostname\nhostname\npwd\n"
 NODES_TEXT = open(os.path.join(GOLD, "c1_scontrol_show_nodes.txt")).read()

@@ -2,7 +2,8 @@
 produce — overlapping and empty partition masks, nodes in no partition, zero and oversized
 demands, partition limits, multi-node jobs up to kmax, tiny windows, timelines with random release
 events — placed by the HIP engines and compared bit-exactly with the oracle (placements, start
-slots, final node state / timelines).  Seeds are fixed, so a failure names its case."""
+slots, final node state / timelines).  Seeds are fixed, so a failure names its case.  Engines by seed: the persistent engine at every
+size (conftest), the host-driven rounds (seed % 4 == 1), the production choice (seed % 4 == 3)."""
 import numpy as np
 import pytest
 
@@ -52,6 +53,8 @@ def random_case(seed, timeline=False):
 def test_fuzz_place(seed, monkeypatch):
     if seed % 4 == 1:  # the host-driven round loop (node-sharded multi-GPU's engine)
         monkeypatch.setenv("FIT_ENGINE", "rounds")
+    elif seed % 4 == 3:  # the production choice: small placements on the rounds, large persistent
+        monkeypatch.delenv("FIT_ENGINE", raising=False)
     nodes, jobs, parts, kmax = random_case(seed)
     r = np.random.default_rng(1000 + seed)
     kw = {} if seed % 3 else {"window_min": int(r.integers(1, 64)), "window_max": int(r.integers(64, 2048))}
@@ -72,6 +75,8 @@ def test_fuzz_place(seed, monkeypatch):
 def test_fuzz_backfill(seed, monkeypatch):
     if seed % 4 == 1:
         monkeypatch.setenv("FIT_ENGINE", "rounds")
+    elif seed % 4 == 3:
+        monkeypatch.delenv("FIT_ENGINE", raising=False)
     nodes, tl, jobs, parts = random_case(100 + seed, timeline=True)
     rn, rs, rst, rfin = po.ref_place_tl(nodes, tl, jobs, parts)
     with Engine() as e:
