@@ -97,9 +97,10 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c5", "c2a", "c3a", "c5a", "admit"],
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3o", "c4", "c5", "c2a", "c3a", "c5a", "admit"],
                     help="c3: BASELINE headline (100k x 1M); c3o: c3 + an all-nodes partition (one "
-                         "component); c5: c3 with a 1,024-slot backfill horizon; admit: CreatePod "
+                         "component); c4: GPU-heavy nodes (8 GPUs) with multi-node jobs (--nodes=k, "
+                         "k in {1,2,4,8}, kmax 8); c5: c3 with a 1,024-slot backfill horizon; admit: CreatePod "
                          "admission latency (10 concurrent callers against the c3 node table); c2a / c3a / "
                          "c5a: the same clusters with an array-expanded pending queue (runs of identical "
                          "pods, synth.expand_arrays) — not a BASELINE config")
@@ -184,7 +185,7 @@ def main():
         nodes, tline, jobs, parts = synth.make_c5(shard=shard)
     else:
         nodes, jobs, parts = synth.make_config(a.workload, shard=shard)
-    kmax = 1
+    kmax = 8 if a.workload == "c4" else 1  # C4: --nodes=k up to 8 (FIT_MAX_K)
 
     mode = {"auto": FIT_SHARD_AUTO, "nodes": FIT_SHARD_NODES, "components": FIT_SHARD_COMPONENTS}[a.shard_mode]
     if weak:
@@ -221,7 +222,7 @@ def main():
                T(nodes.part_mask.view(np.int32))]
     d_jobs = [T(jobs.cpu), T(jobs.mem), T(jobs.gpu), T(jobs.wall), T(jobs.part.view(np.int16)),
               T(jobs.nodes_k.view(np.int16))]
-    d_out = torch.empty(jobs.j, dtype=torch.int32, device=dev)
+    d_out = torch.empty(jobs.j * kmax, dtype=torch.int32, device=dev)
     if tl:
         d_rel = [T(x) for x in (tline.off, tline.slot, tline.cpu, tline.mem, tline.gpu)]
         d_start = torch.empty(jobs.j, dtype=torch.int32, device=dev)
@@ -300,7 +301,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a.workload, nodes, jobs, parts, tline if tl else None, a.cpu_scale)
+        cpu = cpu_baseline(a.workload, nodes, jobs, parts, tline if tl else None, a.cpu_scale, kmax)
 
     resolved = s0["placed"] + s0["unplaced"]
     line = {
@@ -348,7 +349,7 @@ def main():
                                                               wn.avail_min, wn.part_mask)))
         wh_jobs = synth.Jobs(*(_pinned(wkeep, x) for x in (wj.cpu, wj.mem, wj.gpu, wj.wall, wj.part,
                                                             wj.nodes_k)))
-        wh_out = _pinned(wkeep, np.zeros(wj.j, np.int32))
+        wh_out = _pinned(wkeep, np.zeros(wj.j * kmax, np.int32))
         if tl:
             wh_tl = synth.Timeline(wt.slots, wt.slot_min,
                                    *(_pinned(wkeep, x) for x in (wt.off, wt.slot, wt.cpu, wt.mem, wt.gpu)))
@@ -359,7 +360,7 @@ def main():
             if tl:
                 weng.load_timeline(wh_tl)
                 return weng.place_tl(wh_jobs, node=wh_out, start=wh_start)[2]
-            return weng.place(wh_jobs, kmax=1, out=wh_out)[1]
+            return weng.place(wh_jobs, kmax=kmax, out=wh_out)[1]
 
         wel, _, _ = timed(step_weak)
         weng.close()
@@ -517,7 +518,7 @@ def admission(a):
     print(json.dumps(line), flush=True)
 
 
-def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
+def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0, kmax=1):
     """The CPU paths on this host (rank 0, N = 1), each on a bounded sample of the same workload
     (per-job cost is flat in J, so each sample's rate stands for the whole stream):
       naive-port                oracle/fitref*.c, every node per job, 1 thread (the SPEC as stated)
@@ -527,8 +528,9 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
       same-algorithm-multicore  the GPU's algorithm on CPU_THREADS threads
       multicore                 component-aware, components on CPU_THREADS threads
     backfill (c5): naive-port, component-aware (dense slot walk), run-length (the GPU's run lists,
-    1 thread) and multicore (run lists, components on threads).  The line's cpu_baseline object is
-    the fastest variant."""
+    1 thread) and multicore (run lists, components on threads).  Multi-node jobs (c4, kmax 8):
+    naive-port, component-aware and multicore (oracle/cpu_baseline.c cpu_place_k: the k smallest
+    keys per job, components on threads).  The line's cpu_baseline object is the fastest variant."""
     from fitgpu import synth
     from oracle import pyoracle as po
     threads = max(1, min(CPU_THREADS, os.cpu_count() or 1))
@@ -557,6 +559,14 @@ def cpu_baseline(workload, nodes, jobs, parts, tline, scale=1.0):
                 ("multicore", threads, m_rle * par,
                  lambda s: po.cpu_place_tl(nodes, tline, s, parts, threads, rle=True)[2],
                  f"oracle/cpu_fast.c cpu_place_tl_rle, {ncomp} components on {threads} threads")]
+    elif kmax > 1:
+        runs = [("naive-port", 1, m_naive, lambda s: po.ref_place(nodes, s, parts, kmax=kmax)[1],
+                 "oracle/fitref.c ref_place (C restatement of the scalar sequential path, every node per job, "
+                 "k smallest keys)"),
+                ("component-aware", 1, m_comp / 2, lambda s: po.cpu_place_k(nodes, s, parts, kmax, 1)[1],
+                 "oracle/cpu_baseline.c cpu_place_k (own component's nodes only, vectorised keys, top-k)"),
+                ("multicore", threads, m_comp / 2 * par, lambda s: po.cpu_place_k(nodes, s, parts, kmax, threads)[1],
+                 f"oracle/cpu_baseline.c cpu_place_k, {ncomp} components on {threads} threads")]
     else:
         # split-argmin: every job's scan split over the threads, one barrier per job
         m_split = 3e9 / per_comp * max(1, min(threads, 4))

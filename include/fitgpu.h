@@ -272,7 +272,7 @@ int fit_expand_hostlist(const char* expr, char* buf, int32_t buflen);
  * These are the names to send to the Nodes RPC (Client.Nodes, slurm.go:343-364, which joins them
  * with commas for `scontrol show nodes`); record i of its answer is name i, and a caller must
  * refuse the answer when the record count differs.  Returns the count, FIT_E_PARSE (malformed
- * hostlist), FIT_E_INVAL (a name listed twice, or buf too small). */
+ * hostlist, or a name listed twice), FIT_E_INVAL (buf too small: retry with a larger one). */
 int fit_node_names(const char* entries, int32_t n, char* buf, int32_t buflen);
 
 /* ---- batched admission (CreatePod's call site) -----------------
@@ -294,7 +294,12 @@ typedef struct {
     int32_t wall_min;
     uint16_t part;     /* partition index (fit_load_partitions order)                       */
     uint16_t nodes_k;  /* --nodes, 0 = 1, <= FIT_MAX_K                                      */
+    uint16_t flags;    /* FIT_REQ_*: set by fit_pod_demand                                   */
+    uint16_t reserved;
 } fit_admit_req;
+/* fit_admit_req.flags: one task of an array job (an --array label or #SBATCH --array): its pod's
+ * one sbatch serves every task, so fit_admitter_script never pins it to the task's nodes */
+#define FIT_REQ_ARRAY 1
 typedef struct {
     int32_t node[FIT_MAX_K]; /* node ids (nodes_k of them, rest -1), or node[0] = FIT_UNPLACED
                                 (no capacity now: retry) / FIT_REJECTED (partition limits)  */

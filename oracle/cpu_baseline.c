@@ -16,7 +16,9 @@
  *                    ~6k-node scan of ~10 µs, so this decomposition dominates it at C3; at one
  *                    component (c3o) both degenerate to the single-thread scan.
  *
- * k = 1 jobs only for the plain fit (C2/C3/c3o); the backfill variant is §2b's one-node search.
+ * cpu_place: k = 1 jobs (C2/C3/c3o).  cpu_place_k: multi-node jobs (config C4, --nodes=k, the
+ * k smallest distinct keys, all or nothing: fitref.c ref_place's rule), components on threads.
+ * The backfill variant is §2b's one-node search.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -277,6 +279,189 @@ int cpu_place(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free
     }
     pthread_mutex_destroy(&T.mu);
     free((void*)T.order);
+    free_comps(&C);
+    return 0;
+}
+
+/* ------------------------------------------------ plain fit with multi-node jobs (config C4) */
+/* every position's key (UINT64_MAX = infeasible) — branch-free so the loop vectorises */
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static void scan_keys(int32_t len, const int32_t* cf, const int32_t* mf, const int32_t* gf,
+                      const int32_t* av, const uint32_t* mk, const int32_t* id, int32_t c, int32_t m,
+                      int32_t g, int32_t w, uint32_t pbit, uint64_t* keys) {
+    for (int32_t i = 0; i < len; i++) {
+        const int32_t dc = cf[i] - c, dm = mf[i] - m, dg = gf[i] - g, da = av[i] - w;
+        const int ok = ((dc | dm | dg | da) >= 0) & ((mk[i] & pbit) != 0);
+        uint32_t gr = (uint32_t)dg, cr = (uint32_t)dc, mr = (uint32_t)dm >> 10;
+        gr = gr > 255u ? 255u : gr;
+        cr = cr > 4095u ? 4095u : cr;
+        mr = mr > 4095u ? 4095u : mr;
+        const uint64_t key = ((uint64_t)((gr << 24) | (cr << 12) | mr) << 32) | (uint32_t)id[i];
+        keys[i] = ok ? key : UINT64_MAX;
+    }
+}
+
+typedef struct {
+    plain_job_t base;
+    const uint16_t* nodes_k;
+    int32_t kmax;
+} k_job_t;
+
+static int32_t pos_of(const int32_t* id, int32_t len, int32_t x) {
+    int32_t lo = 0, hi = len - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (id[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+static void place_component_k(k_job_t* K, int k, int64_t* placed, int64_t* evals) {
+    plain_job_t* T = &K->base;
+    const comps_t* C = T->C;
+    const int32_t nb = C->nb[k], len = C->nb[k + 1] - nb, kmax = K->kmax;
+    int32_t* cf = malloc(sizeof(int32_t) * (len > 0 ? len : 1) * 4);
+    uint32_t* mk = malloc(sizeof(uint32_t) * (len > 0 ? len : 1));
+    uint64_t* keys = malloc(sizeof(uint64_t) * (len > 0 ? len : 1));
+    int32_t *mf = cf + len, *gf = mf + len, *av = gf + len;
+    const int32_t* id = C->nodes + nb;
+    for (int32_t i = 0; i < len; i++) {
+        const int32_t x = id[i];
+        cf[i] = T->cpu_free[x];
+        mf[i] = T->mem_free[x];
+        gf[i] = T->gpu_free[x];
+        av[i] = T->avail[x];
+        mk[i] = T->mask[x];
+    }
+    for (int32_t t = C->jb[k]; t < C->jb[k + 1]; t++) {
+        const int32_t q = C->jobs[t];
+        int kq = K->nodes_k ? K->nodes_k[q] : 1;
+        if (kq == 0) kq = 1;
+        const int32_t c = T->cpu[q], m = T->mem[q], g = T->gpu[q];
+        uint64_t best[64];
+        if (kq == 1) {
+            best[0] = scan_min(len, cf, mf, gf, av, mk, id, c, m, g, T->wall[q], 1u << T->part[q]);
+        } else {  /* the kq smallest keys: one vectorised key pass, then a sorted insertion */
+            scan_keys(len, cf, mf, gf, av, mk, id, c, m, g, T->wall[q], 1u << T->part[q], keys);
+            for (int i = 0; i < kq; i++) best[i] = UINT64_MAX;
+            for (int32_t i = 0; i < len; i++) {
+                const uint64_t key = keys[i];
+                if (key >= best[kq - 1]) continue;
+                int u = kq - 1;
+                while (u > 0 && best[u - 1] > key) {
+                    best[u] = best[u - 1];
+                    u--;
+                }
+                best[u] = key;
+            }
+        }
+        *evals += len;
+        if (best[kq - 1] == UINT64_MAX) continue; /* fewer than kq nodes fit: nothing taken */
+        int32_t* o = T->out + (int64_t)q * kmax;
+        for (int i = 0; i < kq; i++) {
+            const int32_t x = (int32_t)(uint32_t)best[i], a = pos_of(id, len, x);
+            cf[a] -= c;
+            mf[a] -= m;
+            gf[a] -= g;
+            o[i] = x;
+        }
+        ++*placed;
+    }
+    for (int32_t i = 0; i < len; i++) {
+        const int32_t x = id[i];
+        T->cpu_free[x] = cf[i];
+        T->mem_free[x] = mf[i];
+        T->gpu_free[x] = gf[i];
+    }
+    free(cf);
+    free(mk);
+    free(keys);
+}
+
+static void* k_worker(void* arg) {
+    k_job_t* K = arg;
+    plain_job_t* T = &K->base;
+    int64_t placed = 0, evals = 0;
+    for (;;) {
+        const int32_t i = __atomic_fetch_add(&T->next, 1, __ATOMIC_RELAXED);
+        if (i >= T->C->nc) break;
+        place_component_k(K, T->order[i], &placed, &evals);
+    }
+    pthread_mutex_lock(&T->mu);
+    T->placed += placed;
+    T->evals += evals;
+    pthread_mutex_unlock(&T->mu);
+    return NULL;
+}
+
+/* Plain fit with multi-node jobs: out[q * kmax + i] as ref_place writes it (fitref.c:650-712).
+ * stats: placed, unplaced, rejected, evals.  threads <= 1: one thread. */
+int cpu_place_k(int32_t n, int32_t* cpu_free, int32_t* mem_free, int32_t* gpu_free,
+                const int32_t* avail_min, const uint32_t* part_mask, int32_t p,
+                const int32_t* max_time, const int32_t* max_cpus, const int32_t* max_mem, int32_t j,
+                const int32_t* cpu, const int32_t* mem, const int32_t* gpu, const int32_t* wall,
+                const uint16_t* part, const uint16_t* nodes_k, int32_t kmax, int32_t* out,
+                int64_t* stats, int32_t threads) {
+    if (n < 0 || j < 0 || p < 0 || p > 32 || kmax < 1 || kmax > 64) return -1;
+    for (int32_t q = 0; q < j; q++) {
+        const int kq = nodes_k ? (nodes_k[q] ? nodes_k[q] : 1) : 1;
+        if (kq > kmax || cpu[q] < 0 || mem[q] < 0 || gpu[q] < 0 || wall[q] < 0) return -1;
+    }
+    int32_t* code = malloc(sizeof(int32_t) * (j > 0 ? j : 1)); /* per job: -1 or -2 */
+    comps_t C;
+    memset(&C, 0, sizeof C);
+    if (!code || build_comps(&C, n, part_mask, p, max_time, max_cpus, max_mem, j, cpu, mem, wall, part, code)) {
+        free(code);
+        free_comps(&C);
+        return -1;
+    }
+    int64_t rejected = 0;
+    for (int32_t q = 0; q < j; q++) {
+        const int kq = nodes_k ? (nodes_k[q] ? nodes_k[q] : 1) : 1;
+        int32_t* o = out + (int64_t)q * kmax;
+        for (int i = 0; i < kmax; i++) o[i] = -1;
+        if (code[q] == -2) {
+            for (int i = 0; i < kq; i++) o[i] = -2;
+            rejected++;
+        }
+    }
+    free(code);
+    k_job_t K;
+    memset(&K, 0, sizeof K);
+    plain_job_t* T = &K.base;
+    T->C = &C;
+    T->cpu_free = cpu_free;
+    T->mem_free = mem_free;
+    T->gpu_free = gpu_free;
+    T->avail = avail_min;
+    T->mask = part_mask;
+    T->cpu = cpu;
+    T->mem = mem;
+    T->gpu = gpu;
+    T->wall = wall;
+    T->part = part;
+    T->out = out;
+    T->order = lpt_order(&C, comp_work);
+    K.nodes_k = nodes_k;
+    K.kmax = kmax;
+    pthread_mutex_init(&T->mu, NULL);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    int started = 0;
+    for (int i = 1; i < threads; i++)
+        if (pthread_create(&th[started], NULL, k_worker, &K) == 0) started++;
+    k_worker(&K);
+    for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
+    if (stats) {
+        stats[0] = T->placed;
+        stats[1] = j - T->placed - rejected;
+        stats[2] = rejected;
+        stats[3] = T->evals;
+    }
+    pthread_mutex_destroy(&T->mu);
+    free((void*)T->order);
     free_comps(&C);
     return 0;
 }

@@ -151,6 +151,24 @@ def cpu_place(nodes, jobs, parts, threads: int = 1, variant: str = "component"):
     return out, dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3])), (cf, mf, gf)
 
 
+def cpu_place_k(nodes, jobs, parts, kmax: int, threads: int = 1):
+    """Component-aware best fit with multi-node jobs (config C4; oracle/cpu_baseline.c cpu_place_k,
+    components on `threads` threads): same result as ref_place(..., kmax).  Returns (out[J, kmax],
+    stats dict, final (cpu, mem, gpu))."""
+    cf, mf, gf, av, mk, pt, jb, jp, jk = _prep(nodes, jobs, parts)
+    out = np.empty((jobs.j, kmax), np.int32)
+    st = np.zeros(4, np.int64)
+    I32, U32, U16 = C.c_int32, C.c_uint32, C.c_uint16
+    rc = lib().cpu_place_k(
+        I32(nodes.n), _p(cf, I32), _p(mf, I32), _p(gf, I32), _p(av, I32), _p(mk, U32),
+        I32(parts.p), _p(pt[0], I32), _p(pt[1], I32), _p(pt[2], I32),
+        I32(jobs.j), _p(jb[0], I32), _p(jb[1], I32), _p(jb[2], I32), _p(jb[3], I32), _p(jp, U16),
+        _p(jk, U16), I32(kmax), _p(out, I32), _p(st, C.c_int64), I32(threads))
+    if rc != 0:
+        raise ValueError("cpu_place_k: invalid input")
+    return out, dict(placed=int(st[0]), unplaced=int(st[1]), rejected=int(st[2]), evals=int(st[3])), (cf, mf, gf)
+
+
 def cpu_place_tl(nodes, tline, jobs, parts, threads: int = 1, tl=None, rle: bool = False):
     """Component-aware SPEC §2b backfill on `threads` threads (dense slot walk, or run-length
     timelines with rle=True: oracle/cpu_fast.c).  Same result as ref_place_tl."""

@@ -81,6 +81,7 @@ struct Resv {
     int32_t cpu, mem, gpu;
     int32_t loads;            // node-table loads that re-applied it
     bool confirmed;
+    bool array;               // a task of an array job (FIT_REQ_ARRAY): never pinned
     int64_t confirm_gen;      // latest table generation handed out when it was confirmed
     std::shared_ptr<const Names> names;
 };
@@ -260,6 +261,7 @@ void fit_admitter::place_batch(std::vector<Unit*>& b) {
                 Resv r{};
                 r.k = k;
                 r.cpu = q.cpu, r.mem = q.mem_mib, r.gpu = q.gpu;
+                r.array = (q.flags & FIT_REQ_ARRAY) != 0;
                 r.names = names;
                 for (int x = 0; x < FIT_MAX_K; ++x) r.node[x] = x < k ? o.node[x] : -1;
                 for (int x = 0; x < k; ++x) {  // the engine took it: so does the host copy
@@ -513,7 +515,9 @@ int fit_admitter_script(fit_admitter* a, const int64_t* tickets, int32_t n, cons
     for (int32_t i = 0; i < n; ++i)
         if (!a->resv.count(tickets[i])) return fail(FIT_E_INVAL, "fit_admitter_script: unknown ticket");
     const Resv& r = a->resv.at(tickets[0]);
-    bool pin = n == 1 && r.names && r.names->pinnable;
+    // one request of a job that is not an array job (an array's tasks share one sbatch, and a
+    // single request can still be one task of `--array=0-9%1`: --nodelist would pin every task)
+    bool pin = n == 1 && !r.array && r.names && r.names->pinnable;
     for (int i = 0; pin && i < r.k; ++i) {
         if (r.node[i] < 0) pin = false;  // a node left the partition since the admission
         else nm.emplace_back(r.names->name[(size_t)r.node[i]]);

@@ -5,6 +5,7 @@
 // returns FIT_E_PARSE.  Text is handled as ASCII (scontrol output is ASCII).
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -560,7 +561,8 @@ int fit_node_names(const char* entries, int32_t n, char* buf, int32_t buflen) {
     std::vector<sv> views(names.begin(), names.end());
     std::vector<sv> sorted(views);
     std::sort(sorted.begin(), sorted.end());
-    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return FIT_E_INVAL;
+    // (FIT_E_PARSE, not FIT_E_INVAL: callers grow the buffer on FIT_E_INVAL and must not retry this)
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return FIT_E_PARSE;
     return put_names(views, buf, buflen);
 }
 
@@ -723,11 +725,13 @@ int array_parse(const char* array, int64_t* tasks, int64_t* max_running, int64_t
     std::vector<bool> ids;
     for (sv it : split(a, ","))
         if (!array_item(it, ids)) return FIT_E_PARSE;
-    int64_t n = 0;
-    for (bool b : ids) n += b;
+    int64_t n = 0, last = -1;
+    for (size_t x = 0; x < ids.size(); ++x)
+        if (ids[x]) ++n, last = (int64_t)x;
     *tasks = n;
     *max_running = n < limit ? n : limit;
-    *max_id = (int64_t)ids.size() - 1;
+    // the largest id a step actually reaches (`0-1001:3` ends at 999), not the range's bound
+    *max_id = last;
     return FIT_OK;
 }
 
@@ -744,6 +748,30 @@ int fit_array_tasks(const char* array, int64_t* tasks, int64_t* max_running) {
 int32_t fit_set_max_array_size(int32_t n) {
     if (n < 1 || n > (1 << 22)) return FIT_E_INVAL;
     return g_max_array_size.exchange(n);
+}
+
+// Does the script's #SBATCH header (the lines extractBatchResourcesFromScript reads,
+// pkg/slurm-bridge-operator/parse.go:36-46: empty lines and the shebang skipped, the header ends at
+// the first other line) ask for an array (--array[=v] / -a v / -av)?  extractBatchResourcesFromScript
+// ignores it, but sbatch honours it: the pod is then an array job and is never pinned.
+static bool script_has_array(const char* script) {
+    for (const char* p = script; p && *p;) {
+        const char* e = strchr(p, '\n');
+        const sv line(p, e ? (size_t)(e - p) : strlen(p));
+        p = e ? e + 1 : nullptr;
+        if (line.empty() || line.substr(0, 2) == "#!") continue;
+        if (line.substr(0, 7) != "#SBATCH") break;
+        size_t i = 7;
+        while (i < line.size()) {
+            while (i < line.size() && isspace((unsigned char)line[i])) ++i;
+            size_t j = i;
+            while (j < line.size() && !isspace((unsigned char)line[j])) ++j;
+            const sv tok = line.substr(i, j - i);
+            if (tok == "--array" || tok.substr(0, 8) == "--array=" || tok.substr(0, 2) == "-a") return true;
+            i = j;
+        }
+    }
+    return false;
 }
 
 int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t part,
@@ -773,8 +801,10 @@ int fit_pod_demand(const fit_pod_labels* labels, const char* script, uint16_t pa
     // sbatch would refuse the array (ids >= MaxArraySize): no request, so one pod's label can
     // never turn into a batch of millions of tasks
     if (max_id >= g_max_array_size.load()) return FIT_E_INVAL;
+    // an array job (label or #SBATCH --array): its tasks share one sbatch, never pinned
+    const uint16_t fl = ((L.array && L.array[0]) || script_has_array(script)) ? FIT_REQ_ARRAY : 0;
     for (int64_t i = 0; i < running && i < cap; ++i)
-        out[i] = fit_admit_req{priority, cpu, mem, 0, wall, part, k};
+        out[i] = fit_admit_req{priority, cpu, mem, 0, wall, part, k, fl, 0};
     return (int)running;
 }
 

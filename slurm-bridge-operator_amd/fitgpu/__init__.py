@@ -26,7 +26,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (FIT_E_PARSE, FIT_E_STATE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_SHARD_AUTO,
+from ._lib import (FIT_E_PARSE, FIT_E_STATE, FIT_FLAG_COLLECTIVES, FIT_E_UNLIMITED, FIT_REJECTED, FIT_REQ_ARRAY,
+                   FIT_SHARD_AUTO,
                    FIT_SHARD_COMPONENTS, FIT_SHARD_NODES, FIT_TABLE_PIN, FIT_TABLE_STATE, FIT_UNPLACED, FIT_XCHG_ALLGATHER_U64,
                    FIT_XCHG_MAX_I32, FIT_XCHG_MIN_I32, FIT_XCHG_MIN_U64, XCHG_FN, FitAdmitReq, FitAdmitRes, FitError,
                    FitJobResources, FitNode, FitNodeTable, FitOpts, FitPodLabels, FitResources, FitStats, check, lib)
@@ -137,7 +138,7 @@ def node_names(entries: list[str]) -> list[str]:
         buf = C.create_string_buffer(buflen)
         n = lib().fit_node_names(blob, len(entries), buf, buflen)
         if n == FIT_E_PARSE:
-            raise ValueError(f"malformed hostlist {entries!r}")
+            raise ValueError(f"malformed hostlist or a node name listed twice: {entries!r}")
         if n >= 0:
             return [x.decode() for x in buf.raw.split(b"\0")[:n]]
         if buflen > 1 << 28:
@@ -279,8 +280,9 @@ def set_max_array_size(n: int) -> int:
 
 def pod_demand(labels: dict, script: str | None, part: int = 0, priority: int = 0) -> list[tuple]:
     """A pod's admission requests from its labels (keys of POD_LABEL_KEYS' values) and script:
-    [(priority, cpu, mem_mib, gpu, wall_min, part, nodes_k)] — one per array task that may run
-    at once (include/fitgpu.h fit_pod_demand)."""
+    [(priority, cpu, mem_mib, gpu, wall_min, part, nodes_k, flags)] — one per array task that
+    may run at once (include/fitgpu.h fit_pod_demand); flags FIT_REQ_ARRAY marks an array job's
+    tasks (never pinned by Admitter.script)."""
     byname = {v: k for k, v in POD_LABEL_KEYS.items()}
     vals = {byname[k]: str(v).encode() for k, v in labels.items() if k in byname}
     lab = FitPodLabels(*(vals.get(k) for k in ("nodes", "cpus_per_task", "mem_per_cpu", "ntasks_per_node",
@@ -292,7 +294,7 @@ def pod_demand(labels: dict, script: str | None, part: int = 0, priority: int = 
     check(n, "fit_pod_demand")
     out = (FitAdmitReq * n)()
     check(lib().fit_pod_demand(C.byref(lab), scr, part, priority, out, n), "fit_pod_demand")
-    return [(r.priority, r.cpu, r.mem_mib, r.gpu, r.wall_min, r.part, r.nodes_k) for r in out]
+    return [(r.priority, r.cpu, r.mem_mib, r.gpu, r.wall_min, r.part, r.nodes_k, r.flags) for r in out]
 
 
 def script_with_nodelist(script: str, names: list[str], nodes: list[int]) -> str:

@@ -76,7 +76,10 @@ FIT_MAX_K = 8
 class FitAdmitReq(C.Structure):
     _fields_ = [("priority", C.c_int64), ("cpu", C.c_int32), ("mem_mib", C.c_int32),
                 ("gpu", C.c_int32), ("wall_min", C.c_int32), ("part", C.c_uint16),
-                ("nodes_k", C.c_uint16)]
+                ("nodes_k", C.c_uint16), ("flags", C.c_uint16), ("reserved", C.c_uint16)]
+
+
+FIT_REQ_ARRAY = 1  # fit_admit_req.flags: a task of an array job (never pinned)
 
 
 class FitAdmitRes(C.Structure):

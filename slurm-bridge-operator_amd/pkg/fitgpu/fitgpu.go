@@ -401,7 +401,7 @@ func NodeNames(entries []string) ([]string, error) {
 		n := C.fit_node_names((*C.char)(cb), C.int32_t(len(entries)), (*C.char)(unsafe.Pointer(&buf[0])),
 			C.int32_t(size))
 		if n == C.FIT_E_INVAL && size < 1<<24 {
-			continue // buffer too small (or a repeated name: the last try reports it)
+			continue // buffer too small (a repeated name is FIT_E_PARSE: reported at once)
 		}
 		if err := check(n); err != nil {
 			return nil, err

@@ -194,7 +194,7 @@ def test_pod_demand_array_and_maxtime_through_admission():
             (dict(labels, **{fitgpu.POD_LABEL_KEYS["array"]: "0-9%3"}), SAMPLE_SCRIPT.format(t="1:00:00"))]
     reqs = [fitgpu.pod_demand(l, s, 0, prio) for prio, (l, s) in enumerate(pods)]
     assert [len(r) for r in reqs] == [4, 1, 40, 3]
-    assert reqs[0][0] == (0, 3, 1500, 0, 30, 0, 1) and reqs[1][0][4] == 120
+    assert reqs[0][0] == (0, 3, 1500, 0, 30, 0, 1, fitgpu.FIT_REQ_ARRAY) and reqs[1][0][4] == 120
     with Engine() as e:
         e.load_partitions(parts)
         with Admitter(e, max_batch=64, max_wait_us=1000) as adm:

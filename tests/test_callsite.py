@@ -36,6 +36,19 @@ ARRAYS = st.one_of(st.none(), st.sampled_from([
     "1001", "0-1001%2", "5-2000:500"]))
 
 
+def script_has_array(script: str) -> bool:
+    """sbatch's --array / -a in the #SBATCH header (the header rule of parse.go:36-46): the pod is
+    an array job (fit_admit_req.flags FIT_REQ_ARRAY), whatever the demand count."""
+    for line in script.split("\n"):
+        if line == "" or line.startswith("#!"):
+            continue
+        if not line.startswith("#SBATCH"):
+            break
+        if any(t == "--array" or t.startswith("--array=") or t.startswith("-a") for t in line[7:].split()):
+            return True
+    return False
+
+
 def oracle_pod_demand(labels: dict, script, max_array_size: int = 1001):
     raw = [None if labels.get(k) is None else str(labels[k]).encode() for k in KEYS]
     arr = (C.c_char_p * 6)(*raw)
@@ -61,8 +74,9 @@ def test_pod_demand_matches_oracle(script, nodes, cpt, mpc, tpn, array, ntasks, 
         assert rc == n, (labels, script)
         return
     assert rc == 0 and len(got) == n, (labels, script, got, n)
+    arr = bool(labels.get("array")) or (script is not None and script_has_array(script))
     for i, g in enumerate(got[:64]):
-        assert g == (prio, int(ref[i, 0]), int(ref[i, 1]), 0, int(ref[i, 2]), part, int(ref[i, 3]))
+        assert g == (prio, int(ref[i, 0]), int(ref[i, 1]), 0, int(ref[i, 2]), part, int(ref[i, 3]), int(arr))
 
 
 def test_pod_demand_sample_manifest():
@@ -71,17 +85,17 @@ def test_pod_demand_sample_manifest():
     script = "#!/bin/sh\n#SBATCH --nodes=1\nsrun hostname\nhostname\npwd\n"
     labels = {POD_LABEL_KEYS["ntasks"]: "3", POD_LABEL_KEYS["mem_per_cpu"]: "500",
               POD_LABEL_KEYS["cpus_per_task"]: "1"}
-    assert fitgpu.pod_demand(labels, script, 0, 5) == [(5, 3, 1500, 0, 0, 0, 1)]
+    assert fitgpu.pod_demand(labels, script, 0, 5) == [(5, 3, 1500, 0, 0, 0, 1, 0)]
     # --time in the script → walltime minutes (rounded up); an array label → one request per task
     script2 = script.replace("--nodes=1\n", "--nodes=1\n#SBATCH --time=1:30:30\n")
     labels[POD_LABEL_KEYS["array"]] = "1-4"
-    assert fitgpu.pod_demand(labels, script2, 2, 9) == [(9, 3, 1500, 0, 91, 2, 1)] * 4
+    assert fitgpu.pod_demand(labels, script2, 2, 9) == [(9, 3, 1500, 0, 91, 2, 1, 1)] * 4
     # a label overrides the script (a command-line flag beats an #SBATCH line, slurm.go:189-229)
     labels[POD_LABEL_KEYS["nodes"]] = "2"
     labels[POD_LABEL_KEYS["array"]] = "0-9%3"
-    assert fitgpu.pod_demand(labels, script2) == [(0, 2, 1000, 0, 91, 0, 2)] * 3  # ceil(3/2) tasks/node
+    assert fitgpu.pod_demand(labels, script2) == [(0, 2, 1000, 0, 91, 0, 2, 1)] * 3  # ceil(3/2) tasks/node
     # a label strconv.ParseInt rejects is skipped (provider.go logs and goes on)
-    assert fitgpu.pod_demand({POD_LABEL_KEYS["ntasks"]: "three"}, None) == [(0, 1, 1024, 0, 0, 0, 1)]
+    assert fitgpu.pod_demand({POD_LABEL_KEYS["ntasks"]: "three"}, None) == [(0, 1, 1024, 0, 0, 0, 1, 0)]
     with pytest.raises(ValueError):
         fitgpu.pod_demand({POD_LABEL_KEYS["array"]: "1-10:x"}, None)
     with pytest.raises(ValueError):  # the reference panics on a bare last flag (parse.go:58-60)
@@ -119,6 +133,11 @@ def test_pod_demand_max_array_size():
         fitgpu.pod_demand(big, None)
     assert ei.value.code == fitgpu._lib.FIT_E_INVAL and oracle_pod_demand({"array": "0-4194303%3"}, None)[0] == -2
     assert len(fitgpu.pod_demand({POD_LABEL_KEYS["array"]: "0-1000"}, None)) == 1001
+    # a stepped range is bounded by the last id it reaches (0-1001:3 ends at 999)
+    assert len(fitgpu.pod_demand({POD_LABEL_KEYS["array"]: "0-1001:3"}, None)) == 334
+    assert oracle_pod_demand({"array": "0-1001:3"}, None)[0] == 334
+    with pytest.raises(fitgpu.FitError):  # ... and 0-1002:3 reaches 1002
+        fitgpu.pod_demand({POD_LABEL_KEYS["array"]: "0-1002:3"}, None)
     prev = fitgpu.set_max_array_size(4 << 20)
     try:
         assert prev == 1001
@@ -143,9 +162,13 @@ def test_node_names(entries, want):
 
 
 def test_node_names_errors():
-    with pytest.raises(fitgpu.FitError):
-        fitgpu.node_names(["a", "a"])  # a repeated name: no 1:1 record match
-    with pytest.raises(fitgpu.FitError):
+    # a repeated name (no 1:1 record match) is FIT_E_PARSE — not the buffer-too-small FIT_E_INVAL
+    # callers retry on with a larger buffer
+    assert fitgpu.lib().fit_node_names(b"a\0a\0", 2, fitgpu.C.create_string_buffer(64), 64) == fitgpu._lib.FIT_E_PARSE
+    assert fitgpu.lib().fit_node_names(b"a\0b\0", 2, fitgpu.C.create_string_buffer(2), 2) == fitgpu._lib.FIT_E_INVAL
+    with pytest.raises(ValueError):
+        fitgpu.node_names(["a", "a"])
+    with pytest.raises(ValueError):
         fitgpu.node_names(["n[1-3]", "n2"])
     with pytest.raises(ValueError):
         fitgpu.node_names(["n[1-"])

@@ -120,6 +120,37 @@ def test_drain_node_policy():
     assert {"node3", "node6"} <= pinned                    # the operator's choice, documented risk
 
 
+def test_array_task_never_pinned():
+    """an array job whose demand is ONE request (`--array=0-9%1`: one task at
+    a time, or `--array=5`) is still an array — its one sbatch runs every task, so a --nodelist
+    would pin all of them to the node reserved for one.  On a pinnable table (ingest State, and the
+    gRPC table with FIT_TABLE_PIN) such a pod keeps its script; a plain pod is pinned.  The array
+    comes from the label or from the script's own #SBATCH --array."""
+    cols, names = fitgpu.ingest_nodes(NODES_TEXT, ["debug"])
+    base = {fitgpu.POD_LABEL_KEYS["ntasks"]: "1", fitgpu.POD_LABEL_KEYS["mem_per_cpu"]: "500",
+            fitgpu.POD_LABEL_KEYS["cpus_per_task"]: "4"}
+    arr_script = SCRIPT.replace("--nodes=1\n", "--nodes=1\n#SBATCH --array=0-3%1\n")
+    cases = [(dict(base, **{fitgpu.POD_LABEL_KEYS["array"]: "0-9%1"}), SCRIPT, False),
+             (dict(base, **{fitgpu.POD_LABEL_KEYS["array"]: "5"}), SCRIPT, False),
+             (base, arr_script, False),
+             (base, SCRIPT, True)]
+    for state, pin in ((True, False), (False, True)):
+        with Engine() as e:
+            e.load_partitions(UNLIMITED)
+            with Admitter(e, max_batch=16, max_wait_us=100) as adm:
+                adm.load_table(cols, names, state=state, pin=pin)
+                for labels, script, want in cases:
+                    reqs = fitgpu.pod_demand(labels, script, 0, 0)
+                    assert len(reqs) == 1 and reqs[0][7] == (0 if want else fitgpu.FIT_REQ_ARRAY)
+                    g = adm.admit_group(reqs)
+                    assert g[0][0][0] >= 0 and g[0][4] > 0
+                    text, pinned = adm.script([g[0][4]], script)
+                    assert pinned == want, (labels, script)
+                    assert (text == script) != want
+                    if want:
+                        assert _nodelist(text) == [names[g[0][0][0]]]
+
+
 def _oracle_units(nodes, parts, units, kmax=8):
     """Sequential admission of units (lists of requests) in order; a unit takes its nodes only
     when every request of it is placed (fit_admit_group's all or nothing)."""

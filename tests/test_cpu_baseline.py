@@ -4,7 +4,8 @@ oracle/fitref_tl.c:ref_place_tl) — so their throughput is a like-for-like base
   component   oracle/cpu_baseline.c: each job scans its component's nodes, components on threads
   split       oracle/cpu_fast.c: every job's argmin split over the threads (BASELINE.md:22)
   rounds      oracle/cpu_fast.c: the GPU's candidate-list + dirty-set round algorithm on the CPU
-  rle         oracle/cpu_fast.c: SPEC §2b on run-length timelines (the GPU's layout)"""
+  rle         oracle/cpu_fast.c: SPEC §2b on run-length timelines (the GPU's layout)
+  k           oracle/cpu_baseline.c cpu_place_k: multi-node jobs (config C4), components on threads"""
 import numpy as np
 import pytest
 
@@ -36,3 +37,17 @@ def test_cpu_place_tl_matches_oracle(threads, rle):
     n, s, st, tl = po.cpu_place_tl(nodes, tline, jobs, parts, threads=threads, rle=rle)
     assert np.array_equal(n, rn) and np.array_equal(s, rs) and np.array_equal(tl, rtl)
     assert st["placed"] == rst["placed"] and st["rejected"] == rst["rejected"]
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+@pytest.mark.parametrize("nn,jj", [(512, 4000), (4096, 20000)])
+def test_cpu_place_k_matches_oracle(nn, jj, threads):
+    """config C4 (--nodes=k up to 8): the k smallest distinct keys, all or nothing, as ref_place."""
+    nodes, jobs, parts = synth.make_config("c4", nn, jj)
+    assert jobs.nodes_k.max() > 1
+    ref, rst, rfin = po.ref_place(nodes, jobs, parts, kmax=8)
+    out, st, fin = po.cpu_place_k(nodes, jobs, parts, 8, threads)
+    assert np.array_equal(out, ref)
+    assert all(np.array_equal(a, b) for a, b in zip(fin, rfin))
+    assert {k: st[k] for k in ("placed", "unplaced", "rejected")} == \
+        {k: rst[k] for k in ("placed", "unplaced", "rejected")}
