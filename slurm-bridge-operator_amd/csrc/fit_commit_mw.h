@@ -104,7 +104,13 @@ struct alignas(16) MwShared {
     uint32_t pubt;     // job tiles of the window published to the task ring (MwTiles::ring)
     uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer)
     uint32_t trip_arg; // the failed wait's tile / record
+#if FIT_WD_TILE
+    uint32_t pad[1];
+    uint32_t wclk[8];  // per wave: low 32 bits of the realtime its current long wait started (0: none)
+#else
     uint32_t pad[5];
+    uint32_t wclk[0];
+#endif
     MwRec rec[MW_R];
     MwRow rows[UCAP];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
@@ -144,6 +150,32 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+
+// The clock of a wave's long wait, kept in LDS so that a spin loop holds no register for it (the
+// helper loop is at its VGPR limit: a 64-bit clock per wait site made it spill, C3 +2 ms): a spin
+// loop calls this every 1024 spins (an SMEM round trip for the realtime counter); the first call
+// starts the clock.  Low 32 bits of the 100 MHz counter: waits up to 42.9 s (the deadline's range).
+// The loop clears its slot when it ends after a check (wait_clock_end).
+__device__ __forceinline__ bool wait_clock_over(uint32_t* wclk, const uint32_t* wd) {
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) & 7;
+    const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;
+    const uint32_t t0 = __hip_atomic_load(&wclk[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t0 == 0u) {
+        __hip_atomic_store(&wclk[w], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return false;
+    }
+    return now - t0 > __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Waits inside the block (decider <-> helpers) end when the block's own waves progress, and the
+// helpers' cross-block waits (scan tiles) carry the time deadline; these two keep only a spin bound
+// as a last resort (their loop shape is the round-4 one: a time check there measured +1 % / +4 %
+// on C3 in the stamps / plain builds, profiles/r05e_*).
+constexpr unsigned MW_SPIN_LIMIT = 1u << 28;
+__device__ __forceinline__ void wait_clock_end(uint32_t* wclk, unsigned spins) {
+    if (spins >= 1023u)
+        __hip_atomic_store(&wclk[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) & 7], 0u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // A commit wait gave up (uniform call; helper or decider): the block's first failure names its
 // TripSite and argument in `fail` / `trip_arg`; `fail` stops every wave of the block and the
@@ -427,19 +459,24 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
     if (tile < ready) return true;
     if (T.ring && (unsigned)tile + ENGINE_AHEAD > lds_ld(&S->pubt))
         mw_publish(T, S, min((unsigned)tile + ENGINE_AHEAD, T.ntj));
-    const unsigned long long t0 = realtime();
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-            T.need)
+            T.need) {
+            if (FIT_WD_TILE) wait_clock_end(S->wclk, sp);
             break;
-        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if ((sp & 63u) == 63u && T.ctl && ld_agent(&T.ctl->error)) {  // another block tripped
-            commit_fail(&S->fail, &S->trip_arg, TRIP_PEER, (uint32_t)tile);
-            return false;
         }
-        if (wd_over(sp, t0, lds_ld(&S->wd))) {
+        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
+        if (!FIT_WD_TILE && sp > WD_SPINS) {
             commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
             return false;
+        }
+        if (FIT_WD_TILE && (sp & 1023u) == 1023u) {
+            // (no check of other blocks' trips here: the load of ctl->error made the helper spill,
+            // C3 +2 ms; after a trip elsewhere this wait ends at its own deadline)
+            if (wait_clock_over(S->wclk, &S->wd)) {
+                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
+                return false;
+            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -629,14 +666,12 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
            record slot i & 7's previous one) */                                                \
         uint64_t dn_;                                                                          \
         MW_CLK(hw0_);                                                                          \
-        unsigned long long st0_ = 0ull;                                                        \
         for (unsigned sp_ = 0;; ++sp_) {                                                       \
             dn_ = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   \
             const int lag_ = i - (MW_SNAP - 1) - rfl((int32_t)(uint32_t)dn_);                  \
             if (lag_ <= 0) break;                                                              \
             if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
-            if (sp_ == 0u) st0_ = realtime();                                                  \
-            else if (wd_over(sp_, st0_, lds_ld(&S->wd))) {                                     \
+            if (sp_ > MW_SPIN_LIMIT) {                                                         \
                 commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_SNAP, (uint32_t)i);            \
                 goto hdone;                                                                    \
             }                                                                                  \
@@ -975,11 +1010,10 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
     if (__builtin_expect(!D.exit && (rec_missing || d.stopB || d.full), 0)) {  // the one branch
         if (rec_missing) {  // record t not complete when read: wait for it, read it again
             MW_CLK(c0);
-            const unsigned long long w0 = realtime();
             for (unsigned sp = 0;; ++sp) {
                 flag = lds_ld(&S->rec[t & (MW_R - 1)].h.ready);
                 if (flag == (uint32_t)t + 1u) break;
-                if (lds_ld(&S->fail) || wd_over(sp, w0, lds_ld(&S->wd))) {
+                if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                     commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, (uint32_t)t);
                     D.stop = 3;
                     D.exit = true;
@@ -1092,14 +1126,13 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
     MwRecRegs ra, rb;
     uint32_t flag = 0;
     if (P.w > 0) {
-        const unsigned long long w0 = realtime();
         for (unsigned sp = 0;; ++sp) {
             flag = lds_ld(&S->rec[0].h.ready);
 #ifdef MW_DECIDER_BENCH
             break;
 #endif
             if (flag == 1u) break;
-            if (lds_ld(&S->fail) || wd_over(sp, w0, lds_ld(&S->wd))) {
+            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                 commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, 0u);
                 D.stop = 3;
                 D.exit = true;
@@ -1162,6 +1195,7 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
     if (threadIdx.x < MW_R) S->rec[threadIdx.x].h.ready = 0u;
+    if (FIT_WD_TILE && threadIdx.x < 8) S->wclk[threadIdx.x] = 0u;
     if (threadIdx.x == 0) {
         S->dn = 0ull;
         S->halt = 0u;

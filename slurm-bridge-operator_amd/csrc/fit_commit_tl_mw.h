@@ -75,7 +75,8 @@ struct alignas(16) TmShared {
     uint32_t pubt;     // job tiles of the window published to the task ring (just in time)
     uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer)
     uint32_t trip_arg; // the failed wait's tile / record
-    uint32_t pad[5];
+    uint32_t pad[1];
+    uint32_t wclk[8];  // per wave: its long wait's start (fit_commit_mw.h wait_clock_over)
     TmRec rec[TM_R];
     Seg stage[TM_R][64];     // the run list of each record's first clean item
     TmSlot slot[TL_UCAP];
@@ -135,18 +136,19 @@ __device__ __forceinline__ bool tm_tile_ready(const MwTiles& T, int tt, int& rea
         tm_publish(T, S, min((unsigned)tile + TL_AHEAD, T.ntj));
     const unsigned* tdone = T.tdone;
     const unsigned need = T.need;
-    const unsigned long long t0 = realtime();
     for (unsigned sp = 0;; ++sp) {
-        if (__hip_atomic_load(gview(tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
+        if (__hip_atomic_load(gview(tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) {
+            wait_clock_end(S->wclk, sp);
             break;
-        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if ((sp & 63u) == 63u && T.ctl && ld_agent(&T.ctl->error)) {  // another block tripped
-            commit_fail(&S->fail, &S->trip_arg, TRIP_PEER, (uint32_t)tile);
-            return false;
         }
-        if (wd_over(sp, t0, lds_ld(&S->wd))) {
-            commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
-            return false;
+        if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
+        if ((sp & 1023u) == 1023u) {
+            // (no check of other blocks' trips here: the load of ctl->error made the helper spill,
+            // C3 +2 ms; after a trip elsewhere this wait ends at its own deadline)
+            if (wait_clock_over(S->wclk, &S->wd)) {
+                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
+                return false;
+            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -331,14 +333,12 @@ __device__ __noinline__ void tm_helper(const CompPlan& Pref, TmShared* Sin, Seg*
         // snapshot: the decider has resolved at least t - (TM_M - 1) jobs (so it has read record
         // slot t & 7's previous job)
         uint64_t dn;
-        unsigned long long st0 = 0ull;
         for (unsigned sp = 0;; ++sp) {
             dn = __hip_atomic_load(&S->dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const int lag = t - (TM_M - 1) - rfl((int32_t)(uint32_t)dn);
             if (lag <= 0) break;
             if ((sp & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) return;
-            if (sp == 0u) st0 = realtime();
-            else if (wd_over(sp, st0, lds_ld(&S->wd))) {
+            if (sp > MW_SPIN_LIMIT) {  // within the block: a spin bound only (fit_commit_mw.h)
                 commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_SNAP, (uint32_t)t);
                 return;
             }
@@ -654,11 +654,10 @@ __device__ __forceinline__ void tm_decide(const TmCtx& X, TmDec& D, TmRing& R, T
         if (__builtin_expect(!D.exit && (rec_missing || need_walk || D.gm != 0ull), 0)) {
             if (rec_missing) {  // record t not complete when read: wait for it, read it again
                 TM_CLK(w0);
-                const unsigned long long rw0 = realtime();
                 for (unsigned sp = 0;; ++sp) {
                     flag = lds_ld(&S->rec[t & (TM_R - 1)].h.ready);
                     if (flag == (uint32_t)t + 1u) break;
-                    if (lds_ld(&S->fail) || wd_over(sp, rw0, lds_ld(&S->wd))) {
+                    if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                         commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, (uint32_t)t);
                         D.stop = 3;
                         D.exit = true;
@@ -908,11 +907,10 @@ __device__ __noinline__ CommitResult tm_decider(const CompPlan& Pref, TmShared* 
     const unsigned long long k0 = __builtin_amdgcn_s_memtime();
 #endif
     if (P.w > 0) {
-        const unsigned long long rw0 = realtime();
         for (unsigned sp = 0;; ++sp) {
             flag = lds_ld(&S->rec[0].h.ready);
             if (flag == 1u) break;
-            if (lds_ld(&S->fail) || wd_over(sp, rw0, lds_ld(&S->wd))) {
+            if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
                 commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, 0u);
                 D.stop = 3;
                 D.exit = true;
@@ -977,6 +975,7 @@ __device__ __forceinline__ CommitResult commit_tl_window_mw(
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += SCAN_WAVES * 64) bitmap[i] = 0u;
     if (threadIdx.x < TM_R) S->rec[threadIdx.x].h.ready = 0u;
+    if (threadIdx.x < 8) S->wclk[threadIdx.x] = 0u;
     if (threadIdx.x == 0) {
         S->dn = 0ull;
         S->halt = 0u;

@@ -21,10 +21,41 @@ constexpr unsigned long long TASK_EXIT = ~0ull;
 // count cannot tell a long legitimate wait (another tenant's kernel holding the CUs) from a hang.
 // The first trip of a launch records where it happened (TripRec); fit_last_error reports it.
 __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
-// checked every 64 spins: the clock read is an SMEM round trip
-__device__ __forceinline__ bool wd_over(unsigned spins, unsigned long long t0, unsigned wd) {
-    return (spins & 63u) == 63u && realtime() - t0 > (unsigned long long)wd;
-}
+// The clock of one wait, free while the wait is short: it is read every 64 spins only (an SMEM
+// round trip), and its first read starts it — a spin costs one scalar compare, so the decider's
+// and the helpers' hot waits keep their round-4 shape.  `wd` (or the LDS word holding it) is read
+// only at a check.
+#ifndef FIT_WD_ROUND
+#define FIT_WD_ROUND 1   // committer round-start wait: time deadline (0: spin bound; A/B switch)
+#endif
+#ifndef FIT_WD_WORKER
+#define FIT_WD_WORKER 1  // scan worker task wait: time deadline (0: spin bound; A/B switch)
+#endif
+#ifndef FIT_WD_TILE
+#define FIT_WD_TILE 1    // commit helpers' tile waits: time deadline (0: spin bound; A/B switch)
+#endif
+constexpr unsigned WD_SPINS = 1u << 25;  // the spin bound of a switched-off deadline
+struct WaitClock {
+    unsigned long long t0 = 0ull;
+    __device__ __forceinline__ bool over(unsigned spins, unsigned wd) {
+        if ((spins & 63u) != 63u) return false;
+        const unsigned long long now = realtime();
+        if (t0 == 0ull) {
+            t0 = now;
+            return false;
+        }
+        return now - t0 > (unsigned long long)wd;
+    }
+    __device__ __forceinline__ bool over_lds(unsigned spins, const uint32_t* wd_lds) {
+        if ((spins & 63u) != 63u) return false;
+        const unsigned long long now = realtime();
+        if (t0 == 0ull) {
+            t0 = now;
+            return false;
+        }
+        return now - t0 > (unsigned long long)__hip_atomic_load(wd_lds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
 
 struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
     unsigned q_tail;   // tiles reserved by committers
@@ -176,14 +207,14 @@ __device__ __forceinline__ void release_agent() {
 // rounds with parity p.  false: another block tripped, or this wait outlasted `wd` (recorded).
 __device__ __forceinline__ bool wait_tiles(EngineCtl* ctl, int c, int p, unsigned target,
                                            unsigned wd, unsigned round) {
-    const unsigned long long t0 = realtime();
+    WaitClock clk;
     for (unsigned spins = 0;; ++spins) {
         const unsigned d = ld_agent(&ctl->done[c][2 + p]);
         if (d >= target) return true;
         if (ld_agent(&ctl->error)) return false;
-        if (wd_over(spins, t0, wd)) {
+        if (FIT_WD_ROUND ? clk.over(spins, wd) : spins > WD_SPINS) {
             if ((threadIdx.x & 63u) == 0u)
-                trip_record(ctl, 1u, TRIP_ROUND_START, (unsigned)c, round, target, 0u, d, target, t0);
+                trip_record(ctl, 1u, TRIP_ROUND_START, (unsigned)c, round, target, 0u, d, target, clk.t0);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                                                         __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
             unsigned long long task = TASK_EXIT;
-            const unsigned long long w0 = realtime();
+            WaitClock clk;
             for (unsigned spins = 0;; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
@@ -272,9 +272,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                     break;
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (wd_over(spins, w0, wd)) {
+                if (FIT_WD_WORKER ? clk.over(spins, wd) : spins > WD_SPINS) {
                     trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
-                                (unsigned)ncomp, w0);
+                                (unsigned)ncomp, clk.t0);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);

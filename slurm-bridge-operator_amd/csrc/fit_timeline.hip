@@ -690,10 +690,10 @@ __device__ __forceinline__ CommitResult commit_tl_window(
         if (!tdone) return true;
         const int tile = tt / SCAN_JOBS;
         if (tile < ready) return true;
-        const unsigned long long t0 = realtime();
+        WaitClock clk;
         for (unsigned sp = 0;; ++sp) {
             if (__hip_atomic_load(tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-            if (wd_over(sp, t0, 1000000000u)) return false;  // 10 s
+            if (clk.over(sp, 1000000000u)) return false;  // 10 s
             __builtin_amdgcn_s_sleep(1);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1191,7 +1191,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 held = true;
             }
             const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
-            const unsigned long long w0 = realtime();
+            WaitClock clk;
             for (unsigned spins = 0;; ++spins) {
                 const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
                                                                __ATOMIC_RELAXED,
@@ -1202,9 +1202,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                     break;
                 }
                 if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (wd_over(spins, w0, wd)) {
+                if (clk.over(spins, wd)) {
                     trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
-                                (unsigned)ncomp, w0);
+                                (unsigned)ncomp, clk.t0);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);

@@ -137,7 +137,8 @@ def lib() -> C.CDLL:
         L.fit_destroy.argtypes = [P]
         L.fit_destroy.restype = None
         L.fit_nccl_unique_id.argtypes = [P]
-        L.fit_set_watchdog_us.argtypes = [P, i64]
+        if hasattr(L, "fit_set_watchdog_us"):  # (absent from pre-round-5 variant builds, FITGPU_LIB)
+            L.fit_set_watchdog_us.argtypes = [P, i64]
         for name in ("fit_load_nodes", "fit_load_nodes_device"):
             getattr(L, name).argtypes = [P, i32, P, P, P, P, P]
         L.fit_load_partitions.argtypes = [P, i32, P, P, P]

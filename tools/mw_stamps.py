@@ -8,6 +8,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "slurm-bridge-operator_amd")]
 from fitgpu import _lib  # noqa: E402
 _lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu",
                              sys.argv[2] if len(sys.argv) > 2 else "libfitgpu_stamps.so")
+if len(sys.argv) > 2 and os.path.sep in sys.argv[2]:  # a variant build elsewhere in the tree
+    _lib.LIB_PATH = os.path.join(ROOT, sys.argv[2])
 from fitgpu import Engine, synth  # noqa: E402
 
 W = 24  # stamps per component (MW_NSTAMP)
