@@ -615,7 +615,9 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     HIP_TRY(hipMemsetAsync(c->bnd.p, 0xff, sizeof(uint64_t) * 2 * nc * wcap, st));
     // the node rows as they were: a trip leaves them partly committed, and the context must stay
     // usable after FIT_E_HIP (restored below)
-    HIP_TRY(hipMemcpyAsync(c->rec_bak.p, c->rec.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
+    static const bool no_backup = getenv("FIT_REC_BACKUP") && atoi(getenv("FIT_REC_BACKUP")) == 0;  // A/B only
+    if (!no_backup)
+        HIP_TRY(hipMemcpyAsync(c->rec_bak.p, c->rec.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
     {
         ArbGuard arb;  // one persistent launch per device at a time (see DevArb)
         int rc = arb.take(c->device);

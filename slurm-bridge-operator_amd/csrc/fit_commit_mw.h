@@ -102,15 +102,10 @@ struct alignas(16) MwShared {
     uint32_t fail;     // helper / decider watchdog: the TripSite of the first wait that gave up
     int32_t res[4];    // CommitResult of the window
     uint32_t pubt;     // job tiles of the window published to the task ring (MwTiles::ring)
-    uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer)
+    uint32_t wd;       // watchdog: realtime ticks a wait may last (set by the committer; the
+                       // commit's own waits use spin bounds, see MW_SPIN_LIMIT)
     uint32_t trip_arg; // the failed wait's tile / record
-#if FIT_WD_TILE
-    uint32_t pad[1];
-    uint32_t wclk[8];  // per wave: low 32 bits of the realtime its current long wait started (0: none)
-#else
     uint32_t pad[5];
-    uint32_t wclk[0];
-#endif
     MwRec rec[MW_R];
     MwRow rows[UCAP];
     uint32_t bitmap[1];  // (ne - nb + 31) / 32 words, dirty membership by position
@@ -151,42 +146,26 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
 
-// The clock of a wave's long wait, kept in LDS so that a spin loop holds no register for it (the
-// helper loop is at its VGPR limit: a 64-bit clock per wait site made it spill, C3 +2 ms): a spin
-// loop calls this every 1024 spins (an SMEM round trip for the realtime counter); the first call
-// starts the clock.  Low 32 bits of the 100 MHz counter: waits up to 42.9 s (the deadline's range).
-// The loop clears its slot when it ends after a check (wait_clock_end).
-__device__ __forceinline__ bool wait_clock_over(uint32_t* wclk, const uint32_t* wd) {
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) & 7;
-    const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;
-    const uint32_t t0 = __hip_atomic_load(&wclk[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (t0 == 0u) {
-        __hip_atomic_store(&wclk[w], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return false;
-    }
-    return now - t0 > __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Waits inside the block (decider <-> helpers) end when the block's own waves progress, and the
-// helpers' cross-block waits (scan tiles) carry the time deadline; these two keep only a spin bound
-// as a last resort (their loop shape is the round-4 one: a time check there measured +1 % / +4 %
-// on C3 in the stamps / plain builds, profiles/r05e_*).
-constexpr unsigned MW_SPIN_LIMIT = 1u << 28;
-__device__ __forceinline__ void wait_clock_end(uint32_t* wclk, unsigned spins) {
-    if (spins >= 1023u)
-        __hip_atomic_store(&wclk[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) & 7], 0u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+// The commit's waits — the helpers' waits for scan tiles, and the decider <-> helper waits inside
+// the block — keep round 4's spin bound (MW_SPIN_LIMIT polls, ≈ 4-8 s).  Every other wait of the
+// engine has a time deadline (fit_engine_ctl.h WaitClock), and those bound what the commit waits
+// for: its tiles come from scan workers whose own waits trip on time and drain the launch.  A time
+// check in the helper's tile-wait loop — any extra branch there, in fact — changes the code LLVM
+// generates for the whole (VGPR-limited) helper (different unrolling and branch layout) and cost
+// C3 +0.55 ms / C2 +0.3 ms in paired A/Bs (profiles/r05_watchdog_ab.txt); so the loop keeps its
+// round-4 shape and only the failing branch records its site.
+constexpr unsigned MW_SPIN_LIMIT = 1u << 24;
 
 // A commit wait gave up (uniform call; helper or decider): the block's first failure names its
 // TripSite and argument in `fail` / `trip_arg`; `fail` stops every wave of the block and the
 // committer turns it into the launch's trip record (fit_engine_ctl.h trip_record).
+// Every lane stores the same values (no lane test: a lane id kept live for it cost the decider a
+// VGPR across its whole loop); two waves failing at once may leave the later one's site.
 __device__ __forceinline__ void commit_fail(uint32_t* fail, uint32_t* trip_arg, uint32_t site,
                                             uint32_t arg) {
-    if ((threadIdx.x & 63u) == 0u) {
-        uint32_t none = 0u;
-        if (__hip_atomic_compare_exchange_strong(fail, &none, site, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
-            lds_st(trip_arg, arg);
+    if (lds_ld(fail) == 0u) {
+        lds_st(trip_arg, arg);
+        lds_st(fail, site);
     }
 }
 
@@ -461,22 +440,13 @@ __device__ __forceinline__ bool mw_tile_ready(const MwTiles& T, int tt, int& rea
         mw_publish(T, S, min((unsigned)tile + ENGINE_AHEAD, T.ntj));
     for (unsigned sp = 0;; ++sp) {
         if (__hip_atomic_load(gview(T.tdone) + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-            T.need) {
-            if (FIT_WD_TILE) wait_clock_end(S->wclk, sp);
+            T.need)
             break;
-        }
         if (lds_ld(&S->halt) | lds_ld(&S->fail)) return false;
-        if (!FIT_WD_TILE && sp > WD_SPINS) {
-            commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
+        if (sp > MW_SPIN_LIMIT) {
+            lds_st(&S->trip_arg, (uint32_t)tile);
+            lds_st(&S->fail, TRIP_HELPER_TILE);
             return false;
-        }
-        if (FIT_WD_TILE && (sp & 1023u) == 1023u) {
-            // (no check of other blocks' trips here: the load of ctl->error made the helper spill,
-            // C3 +2 ms; after a trip elsewhere this wait ends at its own deadline)
-            if (wait_clock_over(S->wclk, &S->wd)) {
-                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_TILE, (uint32_t)tile);
-                return false;
-            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -672,7 +642,7 @@ __device__ __forceinline__ uint32_t wave_min32_all(uint32_t v) {
             if (lag_ <= 0) break;                                                              \
             if ((sp_ & 7u) == 7u && (lds_ld(&S->halt) | lds_ld(&S->fail))) goto hdone;         \
             if (sp_ > MW_SPIN_LIMIT) {                                                         \
-                commit_fail(&S->fail, &S->trip_arg, TRIP_HELPER_SNAP, (uint32_t)i);            \
+                lds_st(&S->fail, TRIP_HELPER_SNAP);                                            \
                 goto hdone;                                                                    \
             }                                                                                  \
             /* the decider needs ~1k cycles a job: sleep about that long per missing job      \
@@ -1014,7 +984,7 @@ __device__ __forceinline__ void mw_decide(MwShared* S, const CompPlan& P, MwDec&
                 flag = lds_ld(&S->rec[t & (MW_R - 1)].h.ready);
                 if (flag == (uint32_t)t + 1u) break;
                 if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                    commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, (uint32_t)t);
+                    lds_st(&S->fail, TRIP_DECIDER_REC);
                     D.stop = 3;
                     D.exit = true;
                     break;
@@ -1133,7 +1103,7 @@ __device__ __noinline__ CommitResult mw_decider(const CompPlan& Pref, MwShared* 
 #endif
             if (flag == 1u) break;
             if (sp > MW_SPIN_LIMIT || lds_ld(&S->fail)) {
-                commit_fail(&S->fail, &S->trip_arg, TRIP_DECIDER_REC, 0u);
+                lds_st(&S->fail, TRIP_DECIDER_REC);
                 D.stop = 3;
                 D.exit = true;
                 break;
@@ -1195,7 +1165,6 @@ __device__ __forceinline__ CommitResult commit_window_mw(const CompPlan& P, MwSh
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = threadIdx.x; i < nwords; i += MW_WAVES * 64) S->bitmap[i] = 0u;
     if (threadIdx.x < MW_R) S->rec[threadIdx.x].h.ready = 0u;
-    if (FIT_WD_TILE && threadIdx.x < 8) S->wclk[threadIdx.x] = 0u;
     if (threadIdx.x == 0) {
         S->dn = 0ull;
         S->halt = 0u;

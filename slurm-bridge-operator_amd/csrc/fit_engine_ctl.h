@@ -31,9 +31,6 @@ __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdg
 #ifndef FIT_WD_WORKER
 #define FIT_WD_WORKER 1  // scan worker task wait: time deadline (0: spin bound; A/B switch)
 #endif
-#ifndef FIT_WD_TILE
-#define FIT_WD_TILE 1    // commit helpers' tile waits: time deadline (0: spin bound; A/B switch)
-#endif
 constexpr unsigned WD_SPINS = 1u << 25;  // the spin bound of a switched-off deadline
 struct WaitClock {
     unsigned long long t0 = 0ull;
@@ -91,8 +88,9 @@ __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
 }
 
 // Record a trip (one lane): the first trip of the launch claims ctl->trip and describes itself;
-// every trip ORs its error bit, which drains all blocks.
-static __device__ __noinline__ void trip_record(EngineCtl* ctl, unsigned bit, unsigned site, unsigned comp,
+// every trip ORs its error bit, which drains all blocks.  Inlined: as a call it made k_engine's
+// worker loop keep more registers (154 -> 159 VGPRs, six more call sites).
+static __device__ __forceinline__ void trip_record(EngineCtl* ctl, unsigned bit, unsigned site, unsigned comp,
                                                unsigned round, unsigned arg, unsigned pubt, unsigned tdone,
                                                unsigned need, unsigned long long t0) {
     if (site != TRIP_PEER &&
@@ -117,6 +115,9 @@ static __device__ __noinline__ void trip_record(EngineCtl* ctl, unsigned bit, un
 }
 // the launch's start stamp (the first block to arrive; one lane per block)
 __device__ __forceinline__ void stamp_start(EngineCtl* ctl) {
+#ifdef FIT_WD_NO_STAMP
+    return;
+#endif
     const unsigned long long now = realtime();
     unsigned long long none = 0ull;
     if (__hip_atomic_load(&ctl->t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull)
