@@ -101,7 +101,8 @@ typedef struct {
     double ms_device;      /* device time of the placement launches (HIP events)             */
     int32_t shard_mode;    /* mode used (FIT_SHARD_NODES / FIT_SHARD_COMPONENTS; 0 if world 1) */
     int32_t components;    /* independent partition components                               */
-    int32_t engine;        /* 1: persistent single-launch engine (k_engine); 0: host-driven rounds */
+    int32_t engine;        /* 1: persistent single-launch engine (k_engine); 0: host-driven rounds; */
+                           /* 2: direct small placement (k_small, <= FIT_SMALL_DIRECT jobs)          */
     int32_t reserved;
     double ms_arb_wait;    /* host time waiting for the device's persistent-launch lock: one   */
                            /* persistent launch per GPU at a time, across contexts and processes */

@@ -45,6 +45,11 @@ size_t joblists_scratch_ints(int32_t nj);
 hipError_t launch_joblists(hipStream_t st, const int8_t* jcomp, int32_t nj, int ncomp,
                            int32_t* scratch, int32_t* g, int32_t* jb, int32_t* mb, int32_t* jl,
                            int32_t* jpk);
+hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C,
+                        const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
+                        const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
+                        const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
+                        int32_t* placed);
 hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
                                const int32_t* gpu, const int32_t* av, const uint32_t* mask,
                                const int32_t* perm, int32_t nn, NodeRec* rec);
@@ -277,6 +282,11 @@ struct fit_ctx {
     // host-driven rounds instead of a whole-chip persistent grid: an admission batch of a few
     // hundred pods is one or two rounds of a few tiles (FIT_SMALL_BATCH)
     int32_t small_batch = 2048;
+    // placements of at most this many jobs run k_small: one launch, the jobs one at a time against
+    // every node of their component, no rounds and one host synchronisation (FIT_SMALL_DIRECT)
+    int32_t small_direct = 64;
+    DBuf<int32_t> small_placed;
+    HBuf<int32_t> h_small;
     int cus = 256;
     DBuf<uint8_t> ectl, ering;
     DBuf<CompState> ecs;
@@ -695,9 +705,49 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
 }
 
 // ------------------------------------------------------------------------ placement
+// A small placement in one launch (k_small, fit_kernels.hip) after the prefilter: the device job
+// lists feed it directly, and the stats come back with the placements (h_out, when the caller
+// holds host memory) in ONE synchronisation.
+int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+                 const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
+                 int32_t* out, int32_t* h_out, fit_stats& S) {
+    const int C = c->ncomp;
+    hipStream_t st = c->st;
+    if (c->jl.ensure(std::max(J, 1)) || c->jpk.ensure(J + 1) ||
+        c->jls.ensure(std::max<size_t>(joblists_scratch_ints(J), 1) + 2 * (C + 1) + 2) ||
+        c->small_placed.ensure(std::max(C, 1)) || c->h_small.ensure(C + 2))
+        return FIT_E_OOM;
+    int32_t* g = c->jls.p + joblists_scratch_ints(J);
+    int32_t* jbd = g + 2;
+    int32_t* mbd = jbd + C + 1;
+    HIP_TRY(launch_joblists(st, c->jcomp.p, J, C, c->jls.p, g, jbd, mbd, c->jl.p, c->jpk.p));
+    SmallComps sc;
+    for (int k = 0; k <= 32; ++k) sc.nb[k] = c->nb[std::min(k, C)];
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    HIP_TRY(launch_small(st, C, c->rec.p, sc, jbd, c->jl.p, cpu, mem, gpu, wall, part, nk, kmax, out,
+                         c->small_placed.p));
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    HIP_TRY(hipMemcpyAsync(c->h_small.p, g, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+    if (C > 0)
+        HIP_TRY(hipMemcpyAsync(c->h_small.p + 2, c->small_placed.p, sizeof(int32_t) * C,
+                               hipMemcpyDeviceToHost, st));
+    if (h_out) HIP_TRY(hipMemcpyAsync(h_out, out, sizeof(int32_t) * J * kmax, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_small.p[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
+    S.rejected = c->h_small.p[0];
+    for (int k = 0; k < C; ++k) S.placed += c->h_small.p[2 + k];
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    S.ms_device = S.ms_commit = ms;
+    S.rounds = C > 0 && J > S.rejected ? 1 : 0;
+    S.components = C;
+    S.engine = 2;
+    return 0;
+}
+
 int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
-               int32_t* out, fit_stats* stats) {
+               int32_t* out, fit_stats* stats, int32_t* h_out = nullptr, bool* h_out_done = nullptr) {
     const double t0 = now_ms();
     fit_stats S;
     memset(&S, 0, sizeof S);
@@ -707,6 +757,15 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     if (c->jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
     HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
                              c->jcomp.p));
+    if (J <= c->small_direct && !c->collective()) {  // a few jobs: one launch, one synchronisation
+        const int rc = place_direct(c, J, cpu, mem, gpu, wall, part, nk, kmax, out, h_out, S);
+        if (rc) return rc;
+        if (h_out_done) *h_out_done = h_out != nullptr;
+        S.unplaced = J - S.placed - S.rejected;
+        S.ms_total = now_ms() - t0;
+        if (stats) *stats = S;
+        return 0;
+    }
     // 2. per-component job lists in priority order (stable)
     const int C = c->ncomp;
     std::vector<int32_t> jb;
@@ -1264,12 +1323,15 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     c->cus = prop.multiProcessorCount;
     if (const char* ev = getenv("FIT_WATCHDOG_MS"))
         c->wd_ticks = (unsigned)std::min<double>(4.29e9, std::max(1.0, atof(ev) * 1e5));
-    // FIT_ENGINE: "rounds" = host-driven rounds always, "persistent" = the persistent engine at
-    // every size; unset = persistent above small_batch jobs (FIT_SMALL_BATCH)
+    // unset FIT_ENGINE: k_small up to small_direct jobs, the host-driven rounds up to small_batch
+    // live jobs, the persistent engine above (FIT_SMALL_DIRECT, FIT_SMALL_BATCH)
     if (const char* ev = getenv("FIT_SMALL_BATCH")) c->small_batch = atoi(ev);
+    if (const char* ev = getenv("FIT_SMALL_DIRECT")) c->small_direct = atoi(ev);
+    // FIT_ENGINE forces one engine at every size: "rounds", "persistent" or "direct" (k_small)
     if (const char* ev = getenv("FIT_ENGINE")) {
         c->persistent = strcmp(ev, "rounds") != 0;
         if (strcmp(ev, "persistent") == 0) c->small_batch = -1;
+        c->small_direct = strcmp(ev, "direct") == 0 ? INT32_MAX : -1;
     }
     c->rank = o.rank;
     c->world = o.world;
@@ -1424,9 +1486,11 @@ int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, con
     HIP_TRY(hipMemcpyAsync(c->jpart.p, part, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
     if (nk)
         HIP_TRY(hipMemcpyAsync(c->jk.p, nk, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
+    bool done = false;
     rc = place_impl(c, j, c->jcpu.p, c->jmem.p, c->jgpu.p, c->jwall.p, c->jpart.p,
-                    nk ? c->jk.p : nullptr, kmax, c->out.p, stats);
+                    nk ? c->jk.p : nullptr, kmax, c->out.p, stats, out, &done);
     if (rc) return rc;
+    if (done) return 0;  // the direct small placement copied the placements back with its stats
     HIP_TRY(hipMemcpyAsync(out, c->out.p, sizeof(int32_t) * j * kmax, hipMemcpyDeviceToHost,
                            c->st));
     HIP_TRY(hipStreamSynchronize(c->st));

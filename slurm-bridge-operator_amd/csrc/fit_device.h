@@ -141,6 +141,11 @@ struct CommitResult {
     int32_t placed;
 };
 
+// Component node offsets for the direct small placement (k_small): nb[c] .. nb[c + 1].
+struct SmallComps {
+    int32_t nb[33];
+};
+
 // Persistent engines' watchdog trip record (fit_engine_ctl.h; read back by engine.cpp).
 enum TripSite : unsigned {
     TRIP_NONE = 0,

@@ -278,6 +278,95 @@ hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, N
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------- direct small placement
+// A placement of a few jobs (an admission batch: fit_admitter coalesces the PodSyncWorkers'
+// CreatePod calls, a handful of pods at a time) in ONE launch, no host round trip (DESIGN.md
+// §3.9): block c owns partition component c and walks its jobs (device job list jl[jb[c] ..
+// jb[c+1]), priority order) one at a time, each against every node of the component — SPEC §2
+// directly, no candidate lists, no rounds.  Per job: every thread keeps the minimum key of its
+// strided nodes, a wave DPP minimum then an LDS minimum over the 8 waves gives the block's; a
+// multi-node job takes its k smallest distinct keys by k such extractions (each excludes the keys
+// already taken: keys are unique), all or nothing.  The chosen rows are updated in place in `rec`
+// by the threads that hold the choice; the block barrier makes them visible to the next job's
+// scan (same workgroup).  Cost per job ≈ one pass over the component's rows (L2-resident) and
+// 2 barriers per extraction: a few microseconds, so it is used only for small placements
+// (engine.cpp small_direct) — a large one goes through the rounds.
+constexpr int SMALL_THREADS = 512;
+__global__ __launch_bounds__(SMALL_THREADS) void k_small(
+    NodeRec* rec, SmallComps C, const int32_t* __restrict__ jb, const int32_t* __restrict__ jl,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t kmax,
+    int32_t* __restrict__ out, int32_t* __restrict__ placed) {
+    __shared__ uint64_t wmin[SMALL_THREADS / 64];
+    __shared__ int32_t sel[FIT_KMAX];
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = C.nb[c], ne = C.nb[c + 1];
+    const int t0 = jb[c], t1 = jb[c + 1];
+    int32_t np = 0;  // jobs placed by this block (thread 0)
+    for (int t = t0; t < t1; ++t) {
+        const int q = jl[t];
+        JobRec J;
+        J.q = q;
+        J.cpu = jcpu[q];
+        J.mem = jmem[q];
+        J.gpu = jgpu[q];
+        J.wall = jwall[q];
+        J.pbit = 1u << jpart[q];
+        const int k = jk ? max((int)jk[q], 1) : 1;
+        uint64_t prev = 0ull;  // keys <= prev are taken (extraction r excludes them)
+        uint64_t kth = KEY_INF;
+        for (int r = 0; r < k; ++r) {
+            uint64_t m = KEY_INF;
+            for (int p = nb + (int)threadIdx.x; p < ne; p += SMALL_THREADS) {
+                const NodeRec x = rec[p];
+                const uint64_t key = fit_key(x.cpu, x.mem, x.gpu, x.avail, x.mask, (uint32_t)p, J);
+                m = (key < m && (r == 0 || key > prev)) ? key : m;
+            }
+            const uint64_t w = wave_min_key(m);
+            if (lane == 0) wmin[wave] = w;
+            __syncthreads();
+            uint64_t b = wmin[0];
+#pragma unroll
+            for (int i = 1; i < SMALL_THREADS / 64; ++i) b = umin64(b, wmin[i]);
+            __syncthreads();  // wmin is rewritten by the next extraction
+            if (b == KEY_INF) {  // fewer than k nodes fit: nothing is taken
+                kth = KEY_INF;
+                break;
+            }
+            if (m == b) sel[r] = (int32_t)(uint32_t)b;  // the one thread holding it (keys are unique)
+            prev = b;
+            kth = b;
+        }
+        __syncthreads();  // sel[]
+        if (kth != KEY_INF) {
+            if ((int)threadIdx.x < k) {
+                const int p = sel[threadIdx.x];
+                const NodeRec x = rec[p];
+                rec[p].cpu = x.cpu - J.cpu;
+                rec[p].mem = x.mem - J.mem;
+                rec[p].gpu = x.gpu - J.gpu;
+                out[(int64_t)q * kmax + threadIdx.x] = x.orig;
+            }
+            ++np;
+        }
+        __syncthreads();  // the updated rows, before the next job's scan
+    }
+    if (threadIdx.x == 0) placed[c] = np;
+}
+
+hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C,
+                        const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
+                        const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
+                        const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
+                        int32_t* placed) {
+    if (ncomp == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_small, dim3(ncomp), dim3(SMALL_THREADS), 0, st, rec, C, jb, jl, jcpu, jmem,
+                       jgpu, jwall, jpart, jk, kmax, out, placed);
+    return hipGetLastError();
+}
+
 #ifdef FIT_STAMPS
 extern "C" int fit_debug_commit_stamps(unsigned long long* out /* 64 x 8 */) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -2;

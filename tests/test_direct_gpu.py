@@ -1,0 +1,64 @@
+"""k_small — the direct small placement (one launch, jobs one at a time against every node of their
+component) that admission batches run on — bit-exact against the oracle
+(oracle/fitref.c ref_place) at sizes far beyond its production range (FIT_ENGINE=direct forces it
+at every size): the C3 prefix (16 components), one large component (c3o), multi-node jobs up to
+kmax 8 (c4), and the automatic choice at its threshold (FIT_SMALL_DIRECT)."""
+import numpy as np
+import pytest
+
+from fitgpu import Engine, synth
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(nodes, jobs, parts, kmax=1, engine_id=2):
+    ref, rst, rfin = po.ref_place(nodes, jobs, parts, kmax=kmax)
+    with Engine(device=0) as e:
+        e.load_partitions(parts)
+        e.load_nodes(nodes)
+        out, st = e.place(jobs, kmax=kmax)
+        fin = e.read_nodes()
+    assert st["engine"] == engine_id
+    bad = np.flatnonzero((out != ref).any(axis=1))
+    assert bad.size == 0, f"first mismatch at job {bad[0]}: {out[bad[0]]} vs {ref[bad[0]]}"
+    assert all(np.array_equal(a, b) for a, b in zip(fin, rfin))
+    assert (st["placed"], st["unplaced"], st["rejected"]) == (rst["placed"], rst["unplaced"], rst["rejected"])
+    return st
+
+
+@pytest.mark.parametrize("name,nn,jj,kmax", [("c3", 20000, 60000, 1), ("c3o", 8192, 20000, 1),
+                                              ("c4", 4096, 20000, 8), ("c2", 512, 8192, 1)])
+def test_direct_matches_oracle(name, nn, jj, kmax, monkeypatch):
+    monkeypatch.setenv("FIT_ENGINE", "direct")
+    nodes, jobs, parts = synth.make_config(name, nn, jj)
+    _check(nodes, jobs, parts, kmax)
+
+
+@pytest.mark.parametrize("j,want", [(1, 2), (64, 2), (65, 0)])
+def test_direct_threshold(j, want, monkeypatch):
+    """Unset FIT_ENGINE: up to 64 jobs run k_small (engine 2), more the host-driven rounds (0)."""
+    monkeypatch.delenv("FIT_ENGINE", raising=False)
+    nodes, jobs, parts = synth.make_config("c4", 4096, j)
+    _check(nodes, jobs, parts, kmax=8, engine_id=want)
+
+
+def test_direct_consecutive_batches(monkeypatch):
+    """Admission-sized batches one after the other on one context: each sees the table the
+    previous ones left (the oracle places the concatenated queue)."""
+    monkeypatch.delenv("FIT_ENGINE", raising=False)
+    nodes, jobs, parts = synth.make_config("c3", 20000, 640)
+    ref, _, rfin = po.ref_place(nodes, jobs, parts)
+    got = []
+    with Engine(device=0) as e:
+        e.load_partitions(parts)
+        e.load_nodes(nodes)
+        for b in range(0, 640, 10):
+            sub = synth.Jobs(*(x[b:b + 10] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part,
+                                                     jobs.nodes_k)))
+            out, st = e.place(sub)
+            assert st["engine"] == 2
+            got.append(out)
+        fin = e.read_nodes()
+    assert np.array_equal(np.concatenate(got), ref)
+    assert all(np.array_equal(a, b) for a, b in zip(fin, rfin))

@@ -3,7 +3,8 @@ produce — overlapping and empty partition masks, nodes in no partition, zero a
 demands, partition limits, multi-node jobs up to kmax, tiny windows, timelines with random release
 events — placed by the HIP engines and compared bit-exactly with the oracle (placements, start
 slots, final node state / timelines).  Seeds are fixed, so a failure names its case.  Engines by seed: the persistent engine at every
-size (conftest), the host-driven rounds (seed % 4 == 1), the production choice (seed % 4 == 3)."""
+size (conftest), the host-driven rounds (seed % 4 == 1), the direct small placement k_small at
+every size (seed % 8 == 2), the production choice by size (seed % 4 == 3)."""
 import numpy as np
 import pytest
 
@@ -53,7 +54,9 @@ def random_case(seed, timeline=False):
 def test_fuzz_place(seed, monkeypatch):
     if seed % 4 == 1:  # the host-driven round loop (node-sharded multi-GPU's engine)
         monkeypatch.setenv("FIT_ENGINE", "rounds")
-    elif seed % 4 == 3:  # the production choice: small placements on the rounds, large persistent
+    elif seed % 8 == 2:  # k_small, the admission batches' one-launch placement, at every size
+        monkeypatch.setenv("FIT_ENGINE", "direct")
+    elif seed % 4 == 3:  # the production choice by size (direct / rounds / persistent)
         monkeypatch.delenv("FIT_ENGINE", raising=False)
     nodes, jobs, parts, kmax = random_case(seed)
     r = np.random.default_rng(1000 + seed)
