@@ -14,6 +14,7 @@ from fitgpu import Engine, synth  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c4"
 nodes, jobs, parts = synth.make_config(name, None, int(sys.argv[2]) if len(sys.argv) > 2 else None)
+os.environ["FIT_ENGINE"] = "rounds"  # the host-driven k_commit: its stamps are the ones read back
 with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
