@@ -6,7 +6,9 @@
  * against S_t (in parallel, as 8-lane groups of one wave would).  Job t+i's speculative choice is
  * VALID when no earlier job of the step wrote its chosen node and every node an earlier job of the
  * step wrote keys above it once updated (the rule that makes it the sequential answer); the step
- * commits the valid prefix.  Output: the histogram of committed jobs per step.
+ * commits the valid prefix.  Output: the histogram of committed jobs per step, and why a step
+ * ended early (cause[0]: the job's best node is one an earlier job of the step took — best fit
+ * keeps packing the same node; cause[1]: a node an earlier job took now fits it tighter).
  *
  *   gcc -O2 -shared -fPIC -o tools/libspec_model.so tools/spec_model.c */
 #include <stdint.h>
@@ -28,7 +30,7 @@ static uint64_t key_of(int32_t cf, int32_t mf, int32_t gf, int32_t av, uint32_t 
 int64_t spec_steps(int32_t n, int32_t* cf, int32_t* mf, int32_t* gf, const int32_t* av,
                    const uint32_t* mk, const int32_t* id, int32_t j, const int32_t* c,
                    const int32_t* m, const int32_t* g, const int32_t* w, const uint16_t* part,
-                   int32_t mstep, int64_t* hist, int32_t live_only) {
+                   int32_t mstep, int64_t* hist, int32_t live_only, int64_t* cause) {
     int64_t steps = 0;
     int32_t t = 0;
     int32_t pos[64];
@@ -66,9 +68,13 @@ int64_t spec_steps(int32_t n, int32_t* cf, int32_t* mf, int32_t* gf, const int32
             for (int32_t e = 0; e < i && valid; ++e) {
                 const int32_t x = pos[e];
                 if (x < 0) continue;
-                if (x == pos[i]) valid = 0;
-                else if (key_of(cf[x], mf[x], gf[x], av[x], mk[x], id[x], c[qq], m[qq], g[qq], w[qq], pb) < best[i])
+                if (x == pos[i]) {
                     valid = 0;
+                    if (cause) cause[0]++; /* the node an earlier job of the step took */
+                } else if (key_of(cf[x], mf[x], gf[x], av[x], mk[x], id[x], c[qq], m[qq], g[qq], w[qq], pb) < best[i]) {
+                    valid = 0;
+                    if (cause) cause[1]++; /* a node an earlier job took now fits tighter */
+                }
             }
             if (!valid) break;
             if (pos[i] >= 0) {
