@@ -432,8 +432,8 @@ __device__ unsigned long long g_stamps[64][8];
         const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                      \
         const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime();                  \
         if (threadIdx.x == 0) {                                                           \
-            for (int i_ = 0; i_ < 6; ++i_) g_stamps[c][i_] = st_acc[i_];                  \
-            g_stamps[c][6] = n;                                                           \
+            for (int i_ = 0; i_ < 6; ++i_) g_stamps[c][i_] += st_acc[i_]; /* whole run */ \
+            g_stamps[c][6] += n;                                                          \
             g_stamps[c][7] = ((t1_ - st_t0) << 24) / max(r1_ - st_r0, 1ull); /* cyc/10ns << 24 */ \
         }                                                                                 \
     }
@@ -444,40 +444,72 @@ __device__ unsigned long long g_stamps[64][8];
 #endif
 
 // Multi-node jobs (SPEC k > 1): the K smallest keys among the lane's clean candidate entries and
-// dirty-row keys, ascending, by K wave-wide extractions.  seld[i]: sel[i] is a dirty row.  kth =
-// the K-th key (INF when fewer than K exist).  Returns how many were found.
+// dirty-row keys, ascending.  seld[i]: sel[i] is a dirty row.  kth = the K-th key (INF when fewer
+// than K exist).  Returns how many were found.  Each lane sorts its entries once; then every
+// extraction is a wave minimum of the lane heads — the 32-bit minimum of the scores, then of the
+// positions among the lanes holding it, each as four fused DPP minima and the permlane16 / 32 swaps
+// of gfx950 (in every lane, no readlane, no branch) — and the lane that held it pops its head.
+// Round 5: the previous form (a 64-bit wave minimum over every entry, with a readlane and a tie
+// branch, and a pass clearing the taken key) cost ≈ 500 cycles per extraction at C4
+// (profiles/r05q_c4_stamps.txt).
+#define SK_DPP_MIN(v, CTL) asm volatile("s_nop 1\n\tv_min_u32_dpp %0, %0, %0 " CTL : "+v"(v))
+__device__ __forceinline__ uint32_t sk_wave_min32_all(uint32_t v) {
+    SK_DPP_MIN(v, "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf");
+    SK_DPP_MIN(v, "quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf");
+    SK_DPP_MIN(v, "row_half_mirror row_mask:0xf bank_mask:0xf");
+    SK_DPP_MIN(v, "row_mirror row_mask:0xf bank_mask:0xf");  // every lane: its row's minimum
+    {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = min((uint32_t)p[0], (uint32_t)p[1]);
+    }
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return min((uint32_t)p[0], (uint32_t)p[1]);
+}
+#undef SK_DPP_MIN
 template <int EPL>
 __device__ __forceinline__ int select_k(int K, const uint64_t (&kr)[EPL], const bool (&cl)[EPL],
                                         const uint64_t (&dk)[UPL], uint64_t (&sel)[FIT_KMAX],
                                         bool (&seld)[FIT_KMAX], uint64_t& kth) {
-    uint64_t ce[EPL], de[UPL];
+    constexpr int NE = EPL + UPL;
+    uint64_t q[NE];
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) ce[k] = cl[k] ? kr[k] : KEY_INF;
+    for (int k = 0; k < EPL; ++k) q[k] = cl[k] ? kr[k] : KEY_INF;
 #pragma unroll
-    for (int i = 0; i < UPL; ++i) de[i] = dk[i];
+    for (int i = 0; i < UPL; ++i) q[EPL + i] = dk[i];
+#pragma unroll
+    for (int r = 0; r < NE; ++r)  // odd-even transposition sort, ascending (NE <= 6)
+#pragma unroll
+        for (int i = r & 1; i + 1 < NE; i += 2) {
+            const uint64_t lo = umin64(q[i], q[i + 1]), hi = umax64(q[i], q[i + 1]);
+            q[i] = lo;
+            q[i + 1] = hi;
+        }
     int got = 0;
+    kth = KEY_INF;
 #pragma unroll
     for (int s = 0; s < FIT_KMAX; ++s) {
         sel[s] = KEY_INF;
         seld[s] = false;
-        if (s < K) {
-            uint64_t cmin = KEY_INF, dmin = KEY_INF;
+    }
 #pragma unroll
-            for (int k = 0; k < EPL; ++k) cmin = umin64(cmin, ce[k]);
+    for (int s = 0; s < FIT_KMAX; ++s) {
+        if (s >= K) break;  // uniform
+        const uint32_t hh = (uint32_t)(q[0] >> 32), ll = (uint32_t)q[0];
+        const uint32_t mh = sk_wave_min32_all(hh);
+        const uint32_t ml = sk_wave_min32_all(hh == mh ? ll : 0xffffffffu);
+        const uint64_t b = ((uint64_t)mh << 32) | ml;
+        if (b == KEY_INF) break;  // uniform: fewer than K keys
+        bool d = false;
 #pragma unroll
-            for (int i = 0; i < UPL; ++i) dmin = umin64(dmin, de[i]);
-            const uint64_t b = wave_min_key(umin64(cmin, dmin));
-            if (b != KEY_INF) {
-                sel[s] = b;
-                seld[s] = __ballot(dmin == b) != 0ull;
-                kth = b;
-                ++got;
+        for (int i = 0; i < UPL; ++i) d = d || dk[i] == b;
+        sel[s] = b;
+        seld[s] = __ballot(d) != 0ull;
+        kth = b;
+        ++got;
+        const bool me = q[0] == b;  // keys are unique: one lane pops its head
 #pragma unroll
-                for (int k = 0; k < EPL; ++k) ce[k] = ce[k] == b ? KEY_INF : ce[k];
-#pragma unroll
-                for (int i = 0; i < UPL; ++i) de[i] = de[i] == b ? KEY_INF : de[i];
-            }
-        }
+        for (int e = 0; e + 1 < NE; ++e) q[e] = me ? q[e + 1] : q[e];
+        q[NE - 1] = me ? KEY_INF : q[NE - 1];
     }
     if (got < K) kth = KEY_INF;
     return got;
@@ -542,12 +574,20 @@ struct CRow {  // node row of a candidate (prefetched)
             bool seld_[FIT_KMAX];                                                               \
             uint64_t kth_ = KEY_INF;                                                            \
             const int got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_);            \
+            /* the picks' node rows, lane s holding pick s's: one memory round trip per job */  \
+            uint32_t myp_ = 0u;                                                                 \
+            _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) myp_ =                      \
+                lane == s_ ? (uint32_t)sel_[s_] : myp_;                                         \
+            NodeRec mr_ = {0, 0, 0, 0, 0u, 0, 0, 0};                                            \
+            if (lane < got_) mr_ = rec[myp_];                                                   \
+            STAMP(4);                                                                           \
             if (B != KEY_INF && kth_ > B) {                                                     \
                 stop = 1;                                                                       \
                 goto done;                                                                      \
             }                                                                                   \
             if (got_ == K_) {                                                                   \
                 int nn_ = 0;                                                                    \
+                int32_t pnd_ = -1;                                                              \
                 _Pragma("unroll") for (int i = 0; i < FIT_KMAX; ++i) nn_ += i < K_ && !seld_[i]; \
                 if (nu + nn_ > UCAP) {                                                          \
                     stop = 2;                                                                   \
@@ -570,7 +610,13 @@ struct CRow {  // node row of a candidate (prefetched)
                         nd_ = __builtin_amdgcn_readlane(o, __builtin_ctzll(__ballot(hl_)));     \
                     } else {                                                                    \
                         const uint32_t np_ = (uint32_t)b_;                                      \
-                        const NodeRec r = rec[np_];                                             \
+                        NodeRec r;                                                              \
+                        r.cpu = __builtin_amdgcn_readlane(mr_.cpu, s_);                         \
+                        r.mem = __builtin_amdgcn_readlane(mr_.mem, s_);                         \
+                        r.gpu = __builtin_amdgcn_readlane(mr_.gpu, s_);                         \
+                        r.avail = __builtin_amdgcn_readlane(mr_.avail, s_);                     \
+                        r.mask = (uint32_t)__builtin_amdgcn_readlane((int)mr_.mask, s_);        \
+                        r.orig = __builtin_amdgcn_readlane(mr_.orig, s_);                       \
                         nd_ = r.orig;                                                           \
                         if (lane == (nu & 63)) {                                                \
                             _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i == (nu >> 6)) { \
@@ -590,8 +636,11 @@ struct CRow {  // node row of a candidate (prefetched)
                             cl[N1][k] && (uint32_t)kr[N1][k] != np_;                            \
                     }                                                                           \
                     if (s_ == 0) node = nd_;                                                    \
-                    else if (lane == 0) out[(int64_t)jqr[A] * kmax + s_] = nd_;                 \
+                    else pnd_ = lane == s_ ? nd_ : pnd_;                                        \
                 }                                                                               \
+                /* picks 1..k-1 in one store after the loop: a store counts in vmcnt, so one    \
+                   per pick would make the next pick's row wait for its acknowledgement */      \
+                if (lane > 0 && lane < K_) out[(int64_t)jqr[A] * kmax + lane] = pnd_;           \
                 ++placed;                                                                       \
             }                                                                                   \
         } else {                                                                                \
@@ -665,11 +714,18 @@ struct CRow {  // node row of a candidate (prefetched)
         ++t;                                                                                    \
     }
 
-template <int EPL>
+// BM: the bitmap's pointer type — an LDS (address space 3) pointer when the caller is a device
+// function: through a generic pointer to dynamic LDS, a non-kernel function looks the LDS base up
+// in a table per access (a scalar load and a full lgkmcnt wait, which also drains the job-row
+// prefetch).
+// The array pointers' types likewise: a device-function caller passes global (address space 1)
+// pointers, since through generic ones every access is a flat one, which also counts in lgkmcnt —
+// each LDS wait of a step would then wait for the key and job prefetches too.
+template <int EPL, typename BM, typename RecP, typename CandP, typename JobP, typename OutP>
 __device__ __forceinline__ CommitResult commit_window(
-    int c, const CompPlan& P, NodeRec* __restrict__ rec, const uint64_t* __restrict__ cand,
-    int64_t rank_stride, int nranks, const uint64_t* __restrict__ bnd,
-    const JobRec* __restrict__ wjob, int32_t* __restrict__ out, int kmax, uint32_t* bitmap) {
+    int c, const CompPlan& P, RecP __restrict__ rec, CandP __restrict__ cand,
+    int64_t rank_stride, int nranks, CandP __restrict__ bnd,
+    JobP __restrict__ wjob, OutP __restrict__ out, int kmax, BM bitmap) {
     const int lane = threadIdx.x & 63;
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;
@@ -741,7 +797,7 @@ done:
 #pragma unroll
     for (int i = 0; i < UPL; ++i)
         if (i * 64 + lane < nu) {
-            NodeRec* r = rec + upos[i];
+            const auto r = rec + upos[i];
             r->cpu = ucpu[i];
             r->mem = umem[i];
             r->gpu = ugpu[i];

@@ -29,7 +29,21 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
                                                           const uint64_t* bnd, const JobRec* wjob,
                                                           int32_t* out, int kmax,
                                                           uint32_t* bitmap) {
-    return commit_window<MW_EPL>(c, P, rec, cand, 0, 1, bnd, wjob, out, kmax, bitmap);
+    // the bitmap's LDS address as an opaque SGPR value: seen through, the compiler re-derives it
+    // from the dynamic-LDS offset table at every access (a scalar load + lgkmcnt(0) wait each);
+    // the arrays as global pointers (commit_window: no flat accesses)
+    typedef __attribute__((address_space(3))) uint32_t* LdsWords;
+    uint32_t a = (uint32_t)(uintptr_t)(LdsWords)bitmap;
+    asm volatile("" : "+s"(a));
+#ifdef __HIP_DEVICE_COMPILE__
+#define FIT_GLOBAL(T, p) ((__attribute__((address_space(1))) T*)(p))
+#else  // (the host pass only parses device code)
+#define FIT_GLOBAL(T, p) ((T*)(p))
+#endif
+    return commit_window<MW_EPL>(c, P, FIT_GLOBAL(NodeRec, rec), FIT_GLOBAL(const uint64_t, cand), 0, 1,
+                                 FIT_GLOBAL(const uint64_t, bnd), FIT_GLOBAL(const JobRec, wjob),
+                                 FIT_GLOBAL(int32_t, out), kmax, (LdsWords)(uintptr_t)a);
+#undef FIT_GLOBAL
 }
 
 #ifndef FIT_K0
@@ -446,6 +460,11 @@ extern "C" int fit_debug_tile0(unsigned long long* out /* 8 */) {
 }
 #endif
 #ifdef FIT_STAMPS
+// the single-wave commit's segment stamps of this TU (multi-node windows; fit_common.h STAMP)
+extern "C" int fit_debug_commit_stamps_pe(unsigned long long* out /* 64 x 8 */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fitgpu::g_stamps), sizeof(fitgpu::g_stamps)) ==
+                   hipSuccess ? 0 : -2;
+}
 extern "C" int fit_debug_mw_stamps(unsigned long long* out /* 64 x 16 */) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(fitgpu::g_mw), sizeof(fitgpu::g_mw)) == hipSuccess
                ? 0 : -2;

@@ -1,7 +1,7 @@
 """Diagnostic: per-segment cycles of the single-wave commit (commit_window, fit_common.h) for
-config C4's multi-node windows, from the FIT_STAMPS build (`make stamps`).  The persistent engine
-commits a window holding a multi-node job on wave 0 alone; the stamps of each component's last
-round are read back (fit_debug_commit_stamps)."""
+config C4's multi-node windows, from the FIT_STAMPS build (`make stamps`), summed over the run.  The persistent engine
+commits a window holding a multi-node job on wave 0 alone; argv[3] picks the engine whose
+stamps are read (rounds: k_commit; persistent: engine_commit_single)."""
 import ctypes as C
 import os
 import sys
@@ -13,16 +13,21 @@ _lib.LIB_PATH = os.path.join(ROOT, "slurm-bridge-operator_amd", "fitgpu", "libfi
 from fitgpu import Engine, synth  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c4"
-nodes, jobs, parts = synth.make_config(name, None, int(sys.argv[2]) if len(sys.argv) > 2 else None)
-os.environ["FIT_ENGINE"] = "rounds"  # the host-driven k_commit: its stamps are the ones read back
+nodes, jobs, parts = synth.make_config(name, None, int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] else None)
+eng = sys.argv[3] if len(sys.argv) > 3 else "rounds"
+os.environ["FIT_ENGINE"] = eng  # rounds: k_commit's stamps; persistent: engine_commit_single's
 with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
     _, st = e.place(jobs, kmax=8 if name == "c4" else 1)
     buf = (C.c_ulonglong * (64 * 8))()
-    assert _lib.lib().fit_debug_commit_stamps(buf) == 0
+    rd = _lib.lib().fit_debug_commit_stamps_pe if eng == "persistent" else _lib.lib().fit_debug_commit_stamps
+    assert rd(buf) == 0
 print({k: st[k] for k in ("placed", "unplaced", "rounds", "stops_rescan", "stops_dirty", "ms_device", "ms_commit")})
-names = ["prefetch-issue", "clean-check", "candidate-min", "dirty-eval", "select/decide+update", "rotate+loop"]
+# segments between STAMP(i-1) and STAMP(i) of FIT_COMMIT_STEP (fit_common.h): key loads issued +
+# clean flags of the next job; candidate minimum; dirty-row keys; k = 1: the wave minimum / k > 1:
+# select_k; the decision's bookkeeping (k > 1: the picks' updates); the ring rotation
+names = ["loads+clean-flags", "candidate-min", "dirty-eval", "wave-min | select_k", "decide+update", "rotate+loop"]
 tot = [0] * 6
 jobs_n = 0
 for c in range(64):
@@ -31,6 +36,6 @@ for c in range(64):
     for i in range(6):
         tot[i] += row[i]
 s = sum(tot)
-print(f"last-round jobs {jobs_n}  cycles/job {s / max(jobs_n, 1):.0f}")
+print(f"{eng}: jobs {jobs_n}  cycles/job {s / max(jobs_n, 1):.0f}")
 for n, v in zip(names, tot):
     print(f"  {n:22s} {v / max(jobs_n, 1):8.0f} cycles/job  {100 * v / max(s, 1):5.1f} %")
