@@ -415,8 +415,8 @@ constexpr int UPL = UCAP / 64;  // dirty slots per lane
 
 // ---- diagnostic in-kernel stamps (only in the FIT_STAMPS build; never in the shipped kernel)
 #ifdef FIT_STAMPS
-__device__ unsigned long long g_stamps[64][8];
-#define STAMP_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long st_prev = 0; \
+__device__ unsigned long long g_stamps[64][10];  // [8], [9]: STAMP_CNT2 counters
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_prev = 0; \
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
 #define STAMP(i)                                                                          \
     do {                                                                                  \
@@ -427,6 +427,8 @@ __device__ unsigned long long g_stamps[64][8];
         if (i > 0) st_acc[(i) > 0 ? (i) - 1 : 0] += now_ - st_prev;                                     \
         st_prev = now_;                                                                   \
     } while (0)
+#define STAMP_CNT(x) (st_acc[5] += (x))  // multi-node jobs: dirty-row picks
+#define STAMP_CNT2(a, b) (st_acc[6] += (a), st_acc[7] += (b))
 #define STAMP_FLUSH(c, n)                                                                 \
     {                                                                                     \
         const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                      \
@@ -434,17 +436,22 @@ __device__ unsigned long long g_stamps[64][8];
         if (threadIdx.x == 0) {                                                           \
             for (int i_ = 0; i_ < 6; ++i_) g_stamps[c][i_] += st_acc[i_]; /* whole run */ \
             g_stamps[c][6] += n;                                                          \
+            g_stamps[c][8] += st_acc[6];                                                  \
+            g_stamps[c][9] += st_acc[7];                                                  \
             g_stamps[c][7] = ((t1_ - st_t0) << 24) / max(r1_ - st_r0, 1ull); /* cyc/10ns << 24 */ \
         }                                                                                 \
     }
 #else
 #define STAMP_DECL
 #define STAMP(i)
+#define STAMP_CNT(x)
+#define STAMP_CNT2(a, b)
 #define STAMP_FLUSH(c, n)
 #endif
 
 // Multi-node jobs (SPEC k > 1): the K smallest keys among the lane's clean candidate entries and
-// dirty-row keys, ascending.  seld[i]: sel[i] is a dirty row.  kth = the K-th key (INF when fewer
+// dirty-row keys, ascending.  seld[i]: sel[i] is a dirty row; drank[i]: the pick index of this
+// lane's dirty entry i (-1: not picked).  kth = the K-th key (INF when fewer
 // than K exist).  Returns how many were found.  Each lane sorts its entries once; then every
 // extraction is a wave minimum of the lane heads — the 32-bit minimum of the scores, then of the
 // positions among the lanes holding it, each as four fused DPP minima and the permlane16 / 32 swaps
@@ -469,7 +476,8 @@ __device__ __forceinline__ uint32_t sk_wave_min32_all(uint32_t v) {
 template <int EPL>
 __device__ __forceinline__ int select_k(int K, const uint64_t (&kr)[EPL], const bool (&cl)[EPL],
                                         const uint64_t (&dk)[UPL], uint64_t (&sel)[FIT_KMAX],
-                                        bool (&seld)[FIT_KMAX], uint64_t& kth) {
+                                        bool (&seld)[FIT_KMAX], uint64_t& kth,
+                                        int32_t (&drank)[UPL]) {
     constexpr int NE = EPL + UPL;
     uint64_t q[NE];
 #pragma unroll
@@ -492,6 +500,8 @@ __device__ __forceinline__ int select_k(int K, const uint64_t (&kr)[EPL], const 
         seld[s] = false;
     }
 #pragma unroll
+    for (int i = 0; i < UPL; ++i) drank[i] = -1;
+#pragma unroll
     for (int s = 0; s < FIT_KMAX; ++s) {
         if (s >= K) break;  // uniform
         const uint32_t hh = (uint32_t)(q[0] >> 32), ll = (uint32_t)q[0];
@@ -501,7 +511,11 @@ __device__ __forceinline__ int select_k(int K, const uint64_t (&kr)[EPL], const 
         if (b == KEY_INF) break;  // uniform: fewer than K keys
         bool d = false;
 #pragma unroll
-        for (int i = 0; i < UPL; ++i) d = d || dk[i] == b;
+        for (int i = 0; i < UPL; ++i) {
+            const bool h = dk[i] == b;
+            d = d || h;
+            drank[i] = h ? s : drank[i];
+        }
         sel[s] = b;
         seld[s] = __ballot(d) != 0ull;
         kth = b;
@@ -520,6 +534,28 @@ struct CRow {  // node row of a candidate (prefetched)
     uint32_t mask;
     int32_t orig;
 };
+
+#ifdef FIT_STAMPS
+// diagnostic: the dirty-row keys below the K-th smallest clean key, and jobs with more than 8
+#define STAMP_DIRTY_BELOW(A)                                                                    \
+    {                                                                                           \
+        uint64_t q2_[EPL];                                                                      \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) q2_[k] = cl[A][k] ? kr[A][k] : KEY_INF; \
+        uint64_t t0_ = KEY_INF;                                                                 \
+        for (int s2_ = 0; s2_ < K_; ++s2_) {                                                    \
+            uint64_t m_ = KEY_INF;                                                              \
+            _Pragma("unroll") for (int k = 0; k < EPL; ++k) m_ = umin64(m_, q2_[k]);            \
+            m_ = wave_min_key(m_);                                                              \
+            _Pragma("unroll") for (int k = 0; k < EPL; ++k) q2_[k] = q2_[k] == m_ ? KEY_INF : q2_[k]; \
+            t0_ = m_;                                                                           \
+        }                                                                                       \
+        unsigned long long c2_ = 0;                                                             \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) c2_ += __builtin_popcountll(__ballot(dk[i] < t0_)); \
+        STAMP_CNT2(c2_, c2_ > 8 ? 1ull : 0ull);                                                 \
+    }
+#else
+#define STAMP_DIRTY_BELOW(A)
+#endif
 
 // Pipeline.  Iteration t: vector-load the keys of job t+2; derive the clean
 // flags of job t+1 (bound + dirty bitmap, before job t's commit); resolve job t; clear the flag
@@ -573,13 +609,17 @@ struct CRow {  // node row of a candidate (prefetched)
             uint64_t sel_[FIT_KMAX];                                                            \
             bool seld_[FIT_KMAX];                                                               \
             uint64_t kth_ = KEY_INF;                                                            \
-            const int got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_);            \
+            int32_t drank_[UPL];                                                                \
+            const int got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_, drank_);    \
             /* the picks' node rows, lane s holding pick s's: one memory round trip per job */  \
             uint32_t myp_ = 0u;                                                                 \
             _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) myp_ =                      \
                 lane == s_ ? (uint32_t)sel_[s_] : myp_;                                         \
+            uint32_t cpm_ = 0u; /* the clean picks (the only rows read from memory) */          \
+            _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) cpm_ |=                     \
+                (s_ < got_ && !seld_[s_]) ? 1u << s_ : 0u;                                      \
             NodeRec mr_ = {0, 0, 0, 0, 0u, 0, 0, 0};                                            \
-            if (lane < got_) mr_ = rec[myp_];                                                   \
+            if ((cpm_ >> lane) & 1u) mr_ = rec[myp_];                                           \
             STAMP(4);                                                                           \
             if (B != KEY_INF && kth_ > B) {                                                     \
                 stop = 1;                                                                       \
@@ -589,26 +629,33 @@ struct CRow {  // node row of a candidate (prefetched)
                 int nn_ = 0;                                                                    \
                 int32_t pnd_ = -1;                                                              \
                 _Pragma("unroll") for (int i = 0; i < FIT_KMAX; ++i) nn_ += i < K_ && !seld_[i]; \
+                STAMP_CNT((unsigned long long)(K_ - nn_));                                      \
+                STAMP_DIRTY_BELOW(A);                                                           \
                 if (nu + nn_ > UCAP) {                                                          \
                     stop = 2;                                                                   \
                     goto done;                                                                  \
                 }                                                                               \
-                _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) if (s_ < K_) {         \
+                /* the dirty-row picks (89 % at C4) all at once: each lane updates its picked   \
+                   entries and stores their node ids at their pick index (pick 0: `node`) */     \
+                {                                                                               \
+                    int32_t o0_ = -1;                                                           \
+                    bool h0_ = false;                                                           \
+                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {          \
+                        const int32_t r_ = drank_[i];                                           \
+                        const bool hit_ = r_ >= 0;                                              \
+                        ucpu[i] -= hit_ ? jc : 0;                                               \
+                        umem[i] -= hit_ ? jm : 0;                                               \
+                        ugpu[i] -= hit_ ? jg : 0;                                               \
+                        if (r_ > 0) out[(int64_t)jqr[A] * kmax + r_] = uorig[i];                \
+                        o0_ = r_ == 0 ? uorig[i] : o0_;                                         \
+                        h0_ |= r_ == 0;                                                         \
+                    }                                                                           \
+                    if (seld_[0]) node = __builtin_amdgcn_readlane(o0_, __builtin_ctzll(__ballot(h0_))); \
+                }                                                                               \
+                _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) if (s_ < K_ && !seld_[s_]) { \
                     const uint64_t b_ = sel_[s_];                                               \
                     int32_t nd_;                                                                \
-                    if (seld_[s_]) {                                                            \
-                        int32_t o = 0;                                                          \
-                        bool hl_ = false;                                                       \
-                        _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {      \
-                            const bool hit_ = dk[i] == b_;                                      \
-                            ucpu[i] -= hit_ ? jc : 0;                                           \
-                            umem[i] -= hit_ ? jm : 0;                                           \
-                            ugpu[i] -= hit_ ? jg : 0;                                           \
-                            o = hit_ ? uorig[i] : o;                                            \
-                            hl_ |= hit_;                                                        \
-                        }                                                                       \
-                        nd_ = __builtin_amdgcn_readlane(o, __builtin_ctzll(__ballot(hl_)));     \
-                    } else {                                                                    \
+                    {                                                                           \
                         const uint32_t np_ = (uint32_t)b_;                                      \
                         NodeRec r;                                                              \
                         r.cpu = __builtin_amdgcn_readlane(mr_.cpu, s_);                         \
@@ -640,7 +687,7 @@ struct CRow {  // node row of a candidate (prefetched)
                 }                                                                               \
                 /* picks 1..k-1 in one store after the loop: a store counts in vmcnt, so one    \
                    per pick would make the next pick's row wait for its acknowledgement */      \
-                if (lane > 0 && lane < K_) out[(int64_t)jqr[A] * kmax + lane] = pnd_;           \
+                if (lane > 0 && lane < K_ && pnd_ >= 0) out[(int64_t)jqr[A] * kmax + lane] = pnd_; \
                 ++placed;                                                                       \
             }                                                                                   \
         } else {                                                                                \

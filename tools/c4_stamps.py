@@ -19,23 +19,38 @@ os.environ["FIT_ENGINE"] = eng  # rounds: k_commit's stamps; persistent: engine_
 with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
-    _, st = e.place(jobs, kmax=8 if name == "c4" else 1)
-    buf = (C.c_ulonglong * (64 * 8))()
+    kmax = 8 if name == "c4" else 1
+    out, st = e.place(jobs, kmax=kmax)
+    buf = (C.c_ulonglong * (64 * 10))()
     rd = _lib.lib().fit_debug_commit_stamps_pe if eng == "persistent" else _lib.lib().fit_debug_commit_stamps
     assert rd(buf) == 0
 print({k: st[k] for k in ("placed", "unplaced", "rounds", "stops_rescan", "stops_dirty", "ms_device", "ms_commit")})
 # segments between STAMP(i-1) and STAMP(i) of FIT_COMMIT_STEP (fit_common.h): key loads issued +
 # clean flags of the next job; candidate minimum; dirty-row keys; k = 1: the wave minimum / k > 1:
 # select_k; the decision's bookkeeping (k > 1: the picks' updates); the ring rotation
-names = ["loads+clean-flags", "candidate-min", "dirty-eval", "wave-min | select_k", "decide+update", "rotate+loop"]
+names = ["loads+clean-flags", "candidate-min", "dirty-eval", "wave-min | select_k", "decide+update"]
 tot = [0] * 6
 jobs_n = 0
+below = [0, 0]
 for c in range(64):
-    row = buf[c * 8:(c + 1) * 8]
+    row = buf[c * 10:(c + 1) * 10]
     jobs_n += row[6]
+    below[0] += row[8]
+    below[1] += row[9]
     for i in range(6):
         tot[i] += row[i]
+# [5]: not cycles — the multi-node jobs' picks that were dirty rows (STAMP_CNT)
+dpk = tot[5]
+tot[5] = 0
 s = sum(tot)
+import numpy as np  # noqa: E402
+o = np.asarray(out).reshape(-1, kmax)
+k = np.asarray(jobs.nodes_k).astype(np.int64)
+multi = (k > 1) & (o[:, 0] >= 0)
+picks = int(k[multi].sum())
+print(f"multi-node jobs placed {int(multi.sum())}, picks {picks}, dirty-row picks {dpk} "
+      f"({100 * dpk / max(picks, 1):.1f} %); dirty keys below the k-th clean key per multi-node "
+      f"job {below[0] / max(int(multi.sum()), 1):.2f}, jobs with > 8 of them {below[1]}")
 print(f"{eng}: jobs {jobs_n}  cycles/job {s / max(jobs_n, 1):.0f}")
 for n, v in zip(names, tot):
     print(f"  {n:22s} {v / max(jobs_n, 1):8.0f} cycles/job  {100 * v / max(s, 1):5.1f} %")

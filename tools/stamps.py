@@ -14,13 +14,13 @@ with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
     e.place(jobs)  # last round's commit leaves its stamps
-    buf = (C.c_ulonglong * (64 * 8))()
+    buf = (C.c_ulonglong * (64 * 10))()
     assert _lib.lib().fit_debug_commit_stamps(buf) == 0
 names = ["prefetch-issue", "clean-check", "dirty-eval", "reduction", "decide+update", "rotate+loop"]
 tot = [0] * 6
 jobs_n = 0
 for c in range(64):
-    row = buf[c * 8:(c + 1) * 8]
+    row = buf[c * 10:(c + 1) * 10]
     jobs_n += row[6]
     for i in range(6):
         tot[i] += row[i]
