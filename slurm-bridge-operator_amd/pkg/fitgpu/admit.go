@@ -32,7 +32,12 @@ type Demand struct {
 	WallMin  int32
 	Part     uint16 // partition index in LoadPartitions order
 	NodesK   uint16 // --nodes (0 = 1, <= MaxK)
+	Flags    uint16 // ReqArray: one task of an array job (never pinned to its reserved nodes)
 }
+
+// ReqArray marks a request as one task of an array job (FIT_REQ_ARRAY): PodDemand sets it for a
+// pod with the array label or an `#SBATCH --array` line; Script then never pins it.
+const ReqArray = uint16(C.FIT_REQ_ARRAY)
 
 // Admission is the engine's answer for one request.
 type Admission struct {
@@ -67,7 +72,7 @@ func cReq(d Demand) C.fit_admit_req {
 	return C.fit_admit_req{
 		priority: C.int64_t(d.Priority), cpu: C.int32_t(d.CPU), mem_mib: C.int32_t(d.MemMiB),
 		gpu: C.int32_t(d.GPU), wall_min: C.int32_t(d.WallMin), part: C.uint16_t(d.Part),
-		nodes_k: C.uint16_t(d.NodesK),
+		nodes_k: C.uint16_t(d.NodesK), flags: C.uint16_t(d.Flags),
 	}
 }
 

@@ -353,7 +353,8 @@ func PodDemand(l PodLabels, script string, part uint16, priority int64) ([]Deman
 	out := make([]Demand, len(reqs))
 	for i, r := range reqs {
 		out[i] = Demand{Priority: int64(r.priority), CPU: int32(r.cpu), MemMiB: int32(r.mem_mib),
-			GPU: int32(r.gpu), WallMin: int32(r.wall_min), Part: uint16(r.part), NodesK: uint16(r.nodes_k)}
+			GPU: int32(r.gpu), WallMin: int32(r.wall_min), Part: uint16(r.part), NodesK: uint16(r.nodes_k),
+			Flags: uint16(r.flags)}
 	}
 	return out, nil
 }
