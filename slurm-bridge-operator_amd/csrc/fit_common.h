@@ -536,22 +536,23 @@ struct CRow {  // node row of a candidate (prefetched)
 };
 
 #ifdef FIT_STAMPS
-// diagnostic: the dirty-row keys below the K-th smallest clean key, and jobs with more than 8
+// diagnostic: the size of the candidate set {keys <= T}, T = the smallest per-slice K-th clean key
+// (each block-slice's list is sorted, 16 lanes per slice), and jobs where it is <= 16
 #define STAMP_DIRTY_BELOW(A)                                                                    \
     {                                                                                           \
-        uint64_t q2_[EPL];                                                                      \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) q2_[k] = cl[A][k] ? kr[A][k] : KEY_INF; \
-        uint64_t t0_ = KEY_INF;                                                                 \
-        for (int s2_ = 0; s2_ < K_; ++s2_) {                                                    \
-            uint64_t m_ = KEY_INF;                                                              \
-            _Pragma("unroll") for (int k = 0; k < EPL; ++k) m_ = umin64(m_, q2_[k]);            \
-            m_ = wave_min_key(m_);                                                              \
-            _Pragma("unroll") for (int k = 0; k < EPL; ++k) q2_[k] = q2_[k] == m_ ? KEY_INF : q2_[k]; \
-            t0_ = m_;                                                                           \
+        uint64_t tk_ = KEY_INF;                                                                 \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) {                                       \
+            const uint64_t m_ = __ballot(cl[A][k]);                                             \
+            const uint32_t rm_ = (uint32_t)(m_ >> (lane & 48)) & 0xffffu;                      \
+            const int rk_ = __builtin_popcount(rm_ & ((1u << (lane & 15)) - 1u));               \
+            tk_ = (cl[A][k] && rk_ == K_ - 1) ? umin64(tk_, kr[A][k]) : tk_;                    \
         }                                                                                       \
+        tk_ = wave_min_key(tk_);                                                                \
         unsigned long long c2_ = 0;                                                             \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) c2_ += __builtin_popcountll(__ballot(dk[i] < t0_)); \
-        STAMP_CNT2(c2_, c2_ > 8 ? 1ull : 0ull);                                                 \
+        _Pragma("unroll") for (int k = 0; k < EPL; ++k) c2_ += __builtin_popcountll(__ballot(cl[A][k] && kr[A][k] <= tk_)); \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) c2_ += __builtin_popcountll(__ballot(dk[i] <= tk_)); \
+        if (tk_ == KEY_INF) c2_ = 256;                                                          \
+        STAMP_CNT2(c2_, c2_ <= 16 ? 1ull : 0ull);                                               \
     }
 #else
 #define STAMP_DIRTY_BELOW(A)
