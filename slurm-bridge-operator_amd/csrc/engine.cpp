@@ -226,9 +226,12 @@ DevArb* dev_arb(int device, std::string& err) {
             if (*q == ':' || *q == '/') *q = '_';
         const char* dir = getenv("FIT_LOCK_DIR");
         a->path = std::string(dir && *dir ? dir : "/tmp") + "/fitgpu-" + bus + ".lock";
-        const mode_t um = umask(0);
+        // every user's engines share the file: created 0666 (fchmod, not the process-wide umask);
+        // an existing file of another user in a sticky /tmp may refuse an O_CREAT open
+        // (fs.protected_regular), so it is then opened read-only — flock needs no write access
         a->fd = open(a->path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
-        umask(um);
+        if (a->fd >= 0) (void)fchmod(a->fd, 0666);  // fails harmlessly on another user's file
+        else a->fd = open(a->path.c_str(), O_RDONLY | O_CLOEXEC);
         if (a->fd < 0) {
             err = a->path + ": " + strerror(errno);
             return nullptr;
