@@ -143,26 +143,27 @@ def test_two_processes_mixed_fit_and_backfill(tmp_path):
 def test_lock_file_of_another_user(tmp_path):
     """The device lock file exists and this user cannot write it (another user's file in a sticky
     /tmp refuses an O_CREAT open, fs.protected_regular): the engine opens it read-only — flock
-    needs no write access — and places bit-exactly on the persistent engine."""
+    needs no write access — and places bit-exactly on the persistent engine.  A first child
+    process creates the file; it is then made read-only for the second."""
     if os.geteuid() == 0:
         pytest.skip("root ignores the file mode")
     n1, j1, p1 = synth.make_config("c3", 20000, 60000, shard=1)
     ref = po.ref_place(n1, j1, p1)[0][:, 0]
-    import ctypes
-    bus = ctypes.create_string_buffer(64)
-    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
-    assert hip.hipDeviceGetPCIBusId(bus, 64, 0) == 0
-    name = "fitgpu-" + bus.value.decode().replace(":", "_").replace("/", "_") + ".lock"
-    lock = tmp_path / name
-    lock.write_text("")
-    lock.chmod(0o444)
     env = dict(os.environ, FIT_LOCK_DIR=str(tmp_path), FIT_ENGINE="persistent")
-    out = tmp_path / "fit.npz"
-    p = subprocess.run([sys.executable, os.path.join(HERE, "_two_proc_worker.py"), "fit",
-                        repr(time.time()), "1", str(out)], env=env, stdout=subprocess.PIPE,
-                       stderr=subprocess.STDOUT, timeout=180)
-    assert p.returncode == 0, p.stdout.decode()[-3000:]
-    d = np.load(out)
-    assert (d["engines"] == 1).all()
-    assert np.array_equal(d["res"][0], ref)
-    assert sorted(x.name for x in tmp_path.glob("fitgpu-*.lock")) == [name]  # no second file
+
+    def child(tag):
+        out = tmp_path / f"{tag}.npz"
+        p = subprocess.run([sys.executable, os.path.join(HERE, "_two_proc_worker.py"), "fit",
+                            repr(time.time()), "1", str(out)], env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, timeout=180)
+        assert p.returncode == 0, p.stdout.decode()[-3000:]
+        d = np.load(out)
+        assert (d["engines"] == 1).all()
+        assert np.array_equal(d["res"][0], ref)
+
+    child("first")
+    locks = list(tmp_path.glob("fitgpu-*.lock"))
+    assert len(locks) == 1, locks
+    locks[0].chmod(0o444)
+    child("read_only")
+    assert list(tmp_path.glob("fitgpu-*.lock")) == locks  # the same file, no second one
