@@ -536,23 +536,30 @@ struct CRow {  // node row of a candidate (prefetched)
 };
 
 #ifdef FIT_STAMPS
-// diagnostic: the size of the candidate set {keys <= T}, T = the smallest per-slice K-th clean key
-// (each block-slice's list is sorted, 16 lanes per slice), and jobs where it is <= 16
+// diagnostic: [8] jobs whose fitting dirty rows number <= 16 (and >= K), [9] those among them
+// whose K smallest keys are all dirty rows (no clean key below the K-th dirty key)
 #define STAMP_DIRTY_BELOW(A)                                                                    \
     {                                                                                           \
-        uint64_t tk_ = KEY_INF;                                                                 \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) {                                       \
-            const uint64_t m_ = __ballot(cl[A][k]);                                             \
-            const uint32_t rm_ = (uint32_t)(m_ >> (lane & 48)) & 0xffffu;                      \
-            const int rk_ = __builtin_popcount(rm_ & ((1u << (lane & 15)) - 1u));               \
-            tk_ = (cl[A][k] && rk_ == K_ - 1) ? umin64(tk_, kr[A][k]) : tk_;                    \
+        int nd_ = 0;                                                                            \
+        _Pragma("unroll") for (int i = 0; i < UPL; ++i) nd_ += __builtin_popcountll(__ballot(dk[i] != KEY_INF)); \
+        unsigned long long a_ = 0, b_ = 0;                                                      \
+        if (nd_ <= 16 && nd_ >= K_) {                                                           \
+            a_ = 1;                                                                             \
+            uint64_t q2_[UPL];                                                                  \
+            _Pragma("unroll") for (int i = 0; i < UPL; ++i) q2_[i] = dk[i];                     \
+            uint64_t td_ = KEY_INF;                                                             \
+            for (int s2_ = 0; s2_ < K_; ++s2_) {                                                \
+                uint64_t m_ = KEY_INF;                                                          \
+                _Pragma("unroll") for (int i = 0; i < UPL; ++i) m_ = umin64(m_, q2_[i]);        \
+                m_ = wave_min_key(m_);                                                          \
+                _Pragma("unroll") for (int i = 0; i < UPL; ++i) q2_[i] = q2_[i] == m_ ? KEY_INF : q2_[i]; \
+                td_ = m_;                                                                       \
+            }                                                                                   \
+            int cb_ = 0;                                                                        \
+            _Pragma("unroll") for (int k = 0; k < EPL; ++k) cb_ += __builtin_popcountll(__ballot(cl[A][k] && kr[A][k] < td_)); \
+            b_ = cb_ == 0 ? 1 : 0;                                                              \
         }                                                                                       \
-        tk_ = wave_min_key(tk_);                                                                \
-        unsigned long long c2_ = 0;                                                             \
-        _Pragma("unroll") for (int k = 0; k < EPL; ++k) c2_ += __builtin_popcountll(__ballot(cl[A][k] && kr[A][k] <= tk_)); \
-        _Pragma("unroll") for (int i = 0; i < UPL; ++i) c2_ += __builtin_popcountll(__ballot(dk[i] <= tk_)); \
-        if (tk_ == KEY_INF) c2_ = 256;                                                          \
-        STAMP_CNT2(c2_, c2_ <= 16 ? 1ull : 0ull);                                               \
+        STAMP_CNT2(a_, b_);                                                                     \
     }
 #else
 #define STAMP_DIRTY_BELOW(A)

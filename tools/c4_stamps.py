@@ -49,9 +49,8 @@ k = np.asarray(jobs.nodes_k).astype(np.int64)
 multi = (k > 1) & (o[:, 0] >= 0)
 picks = int(k[multi].sum())
 print(f"multi-node jobs placed {int(multi.sum())}, picks {picks}, dirty-row picks {dpk} "
-      f"({100 * dpk / max(picks, 1):.1f} %); keys <= T (the smallest per-slice k-th clean key; 256 "
-      f"when no slice has k) per multi-node job {below[0] / max(int(multi.sum()), 1):.2f}, jobs "
-      f"with <= 16 of them {below[1]}")
+      f"({100 * dpk / max(picks, 1):.1f} %); jobs with k..16 fitting dirty rows {below[0]}, and of "
+      f"them all k picks dirty {below[1]}")
 print(f"{eng}: jobs {jobs_n}  cycles/job {s / max(jobs_n, 1):.0f}")
 for n, v in zip(names, tot):
     print(f"  {n:22s} {v / max(jobs_n, 1):8.0f} cycles/job  {100 * v / max(s, 1):5.1f} %")
