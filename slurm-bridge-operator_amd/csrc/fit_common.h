@@ -565,6 +565,50 @@ struct CRow {  // node row of a candidate (prefetched)
 #define STAMP_DIRTY_BELOW(A)
 #endif
 
+// Multi-node jobs whose fitting dirty rows number k..16 (46 % of C4's placed multi-node jobs): the
+// k smallest dirty keys by compaction into lanes 0..15 (LDS scratch `scr`, 192 B) and rank by
+// count (each of the ≤ 16 keys broadcast, every lane counts the smaller ones) — no sequential wave
+// minima.  Exact when no clean candidate key is below the k-th dirty key (then the k smallest of
+// all are these; 95 % of the cases): returns true and fills drank / kth, else false (the caller
+// runs select_k).  nd = the number of fitting dirty rows, m0 / m1 their ballots.
+__device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t m1, const uint64_t (&dk)[UPL],
+                                           const uint64_t* kc, const bool* cc, int epl, uint32_t scr,
+                                           int32_t (&drank)[UPL], uint64_t& kth) {
+    static_assert(UPL == 2, "two dirty entries per lane");
+    typedef __attribute__((address_space(3))) uint64_t* L64;
+    typedef __attribute__((address_space(3))) int32_t* L32;
+    const int lane = threadIdx.x & 63;
+    const uint32_t lo0 = (uint32_t)m0, hi0 = (uint32_t)(m0 >> 32), lo1 = (uint32_t)m1, hi1 = (uint32_t)(m1 >> 32);
+    const int p0 = (int)__builtin_amdgcn_mbcnt_hi(hi0, __builtin_amdgcn_mbcnt_lo(lo0, 0u));
+    const int p1 = __builtin_popcountll(m0) + (int)__builtin_amdgcn_mbcnt_hi(hi1, __builtin_amdgcn_mbcnt_lo(lo1, 0u));
+    const bool v0 = dk[0] != KEY_INF, v1 = dk[1] != KEY_INF;
+    L64 keys = (L64)(uintptr_t)scr;
+    L32 ranks = (L32)(uintptr_t)(scr + 128u);
+    if (v0) keys[p0] = dk[0];
+    if (v1) keys[p1] = dk[1];
+    const uint64_t x = lane < nd ? keys[lane & 15] : KEY_INF;  // (one wave: LDS in order)
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // fully unrolled: faster than a loop over nd, or 32 keys
+        const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), j) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
+        r += y < x ? 1 : 0;
+    }
+    const uint64_t kb = __ballot(lane < nd && r == K - 1);
+    const int kl = __builtin_ctzll(kb);
+    const uint64_t t = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), kl) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, kl);
+    bool below = false;
+    for (int k = 0; k < epl; ++k) below = below || (cc[k] && kc[k] < t);
+    if (__ballot(below) != 0ull) return false;  // a clean key among the k smallest
+    if (lane < 16) ranks[lane] = r;
+    const int32_t r0 = v0 ? ranks[p0] : 64, r1 = v1 ? ranks[p1] : 64;
+    drank[0] = r0 < K ? r0 : -1;
+    drank[1] = r1 < K ? r1 : -1;
+    kth = t;
+    return true;
+}
+
 // Pipeline.  Iteration t: vector-load the keys of job t+2; derive the clean
 // flags of job t+1 (bound + dirty bitmap, before job t's commit); resolve job t; clear the flag
 // of any job-(t+1) candidate equal to the node job t dirtied; scalar-load job t+3's row and
@@ -618,7 +662,23 @@ struct CRow {  // node row of a candidate (prefetched)
             bool seld_[FIT_KMAX];                                                               \
             uint64_t kth_ = KEY_INF;                                                            \
             int32_t drank_[UPL];                                                                \
-            const int got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_, drank_);    \
+            int got_;                                                                           \
+            bool fast_ = false;                                                                 \
+            if constexpr (FASTD) {                                                              \
+                const uint64_t fm0_ = __ballot(dk[0] != KEY_INF), fm1_ = __ballot(dk[1] != KEY_INF); \
+                const int fnd_ = __builtin_popcountll(fm0_) + __builtin_popcountll(fm1_);       \
+                if (fnd_ >= K_ && fnd_ <= 16)                                                   \
+                    fast_ = dirty_topk(K_, fnd_, fm0_, fm1_, dk, kr[A], cl[A], EPL, scr, drank_, kth_); \
+            }                                                                                   \
+            if (fast_) {                                                                        \
+                got_ = K_;                                                                      \
+                _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) {                       \
+                    sel_[s_] = KEY_INF;                                                         \
+                    seld_[s_] = true;                                                           \
+                }                                                                               \
+            } else {                                                                            \
+                got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_, drank_);          \
+            }                                                                                   \
             /* the picks' node rows, lane s holding pick s's: one memory round trip per job */  \
             uint32_t myp_ = 0u;                                                                 \
             _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) myp_ =                      \
@@ -776,11 +836,12 @@ struct CRow {  // node row of a candidate (prefetched)
 // The array pointers' types likewise: a device-function caller passes global (address space 1)
 // pointers, since through generic ones every access is a flat one, which also counts in lgkmcnt —
 // each LDS wait of a step would then wait for the key and job prefetches too.
-template <int EPL, typename BM, typename RecP, typename CandP, typename JobP, typename OutP>
+template <int EPL, bool FASTD = false, typename BM, typename RecP, typename CandP, typename JobP,
+          typename OutP>
 __device__ __forceinline__ CommitResult commit_window(
     int c, const CompPlan& P, RecP __restrict__ rec, CandP __restrict__ cand,
     int64_t rank_stride, int nranks, CandP __restrict__ bnd,
-    JobP __restrict__ wjob, OutP __restrict__ out, int kmax, BM bitmap) {
+    JobP __restrict__ wjob, OutP __restrict__ out, int kmax, BM bitmap, uint32_t scr = 0u) {
     const int lane = threadIdx.x & 63;
     const int nwords = (P.ne - P.nb + 31) >> 5;
     for (int i = lane; i < nwords; i += 64) bitmap[i] = 0u;

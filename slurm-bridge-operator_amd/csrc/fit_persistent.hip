@@ -28,7 +28,7 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
                                                           const uint64_t* cand,
                                                           const uint64_t* bnd, const JobRec* wjob,
                                                           int32_t* out, int kmax,
-                                                          uint32_t* bitmap) {
+                                                          uint32_t* bitmap, uint32_t* scratch) {
     // the bitmap's LDS address as an opaque SGPR value: seen through, the compiler re-derives it
     // from the dynamic-LDS offset table at every access (a scalar load + lgkmcnt(0) wait each);
     // the arrays as global pointers (commit_window: no flat accesses)
@@ -40,9 +40,11 @@ __device__ __noinline__ CommitResult engine_commit_single(int c, const CompPlan 
 #else  // (the host pass only parses device code)
 #define FIT_GLOBAL(T, p) ((T*)(p))
 #endif
-    return commit_window<MW_EPL>(c, P, FIT_GLOBAL(NodeRec, rec), FIT_GLOBAL(const uint64_t, cand), 0, 1,
-                                 FIT_GLOBAL(const uint64_t, bnd), FIT_GLOBAL(const JobRec, wjob),
-                                 FIT_GLOBAL(int32_t, out), kmax, (LdsWords)(uintptr_t)a);
+    uint32_t sa = (uint32_t)(uintptr_t)(LdsWords)scratch;  // 256 B of LDS the helpers do not use here
+    asm volatile("" : "+s"(sa));
+    return commit_window<MW_EPL, true>(c, P, FIT_GLOBAL(NodeRec, rec), FIT_GLOBAL(const uint64_t, cand), 0,
+                                       1, FIT_GLOBAL(const uint64_t, bnd), FIT_GLOBAL(const JobRec, wjob),
+                                       FIT_GLOBAL(int32_t, out), kmax, (LdsWords)(uintptr_t)a, sa);
 #undef FIT_GLOBAL
 }
 
@@ -207,7 +209,8 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
             } else {
                 if (wave == 0) {
                     const CommitResult r0 =
-                        engine_commit_single(c, P, rec, cand, bnd, wjob, out, kmax, M->bitmap);
+                        engine_commit_single(c, P, rec, cand, bnd, wjob, out, kmax, M->bitmap,
+                                             reinterpret_cast<uint32_t*>(&M->rows[0]));
                     if (lane == 0) {
                         M->res[0] = r0.done;
                         M->res[1] = r0.stop;
