@@ -720,6 +720,7 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
                     }                                                                           \
                     if (seld_[0]) node = __builtin_amdgcn_readlane(o0_, __builtin_ctzll(__ballot(h0_))); \
                 }                                                                               \
+                if (nn_ > 0) { /* uniform: clean picks (none for most jobs) */                    \
                 _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) if (s_ < K_ && !seld_[s_]) { \
                     const uint64_t b_ = sel_[s_];                                               \
                     int32_t nd_;                                                                \
@@ -756,6 +757,7 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
                 /* picks 1..k-1 in one store after the loop: a store counts in vmcnt, so one    \
                    per pick would make the next pick's row wait for its acknowledgement */      \
                 if (lane > 0 && lane < K_ && pnd_ >= 0) out[(int64_t)jqr[A] * kmax + lane] = pnd_; \
+                }                                                                               \
                 ++placed;                                                                       \
             }                                                                                   \
         } else {                                                                                \
