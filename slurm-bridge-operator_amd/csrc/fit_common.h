@@ -703,22 +703,26 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
                     stop = 2;                                                                   \
                     goto done;                                                                  \
                 }                                                                               \
-                /* the dirty-row picks (89 % at C4) all at once: each lane updates its picked   \
-                   entries and stores their node ids at their pick index (pick 0: `node`) */     \
+                /* the dirty-row picks (89 % at C4) all at once, branch-free: each lane updates \
+                   its picked entries (an entry past nu is never picked: its key is INF) and    \
+                   stores their node ids at their pick index; the other lanes store to the       \
+                   job's pick-0 slot, which the parked placement overwrites later (in order) */  \
                 {                                                                               \
                     int32_t o0_ = -1;                                                           \
                     bool h0_ = false;                                                           \
-                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) if (i * 64 < nu) {          \
+                    const int64_t ob_ = (int64_t)jqr[A] * kmax;                                 \
+                    _Pragma("unroll") for (int i = 0; i < UPL; ++i) {                           \
                         const int32_t r_ = drank_[i];                                           \
                         const bool hit_ = r_ >= 0;                                              \
                         ucpu[i] -= hit_ ? jc : 0;                                               \
                         umem[i] -= hit_ ? jm : 0;                                               \
                         ugpu[i] -= hit_ ? jg : 0;                                               \
-                        if (r_ > 0) out[(int64_t)jqr[A] * kmax + r_] = uorig[i];                \
+                        out[ob_ + (r_ > 0 ? r_ : 0)] = uorig[i];                                \
                         o0_ = r_ == 0 ? uorig[i] : o0_;                                         \
                         h0_ |= r_ == 0;                                                         \
                     }                                                                           \
-                    if (seld_[0]) node = __builtin_amdgcn_readlane(o0_, __builtin_ctzll(__ballot(h0_))); \
+                    const int32_t n0_ = __builtin_amdgcn_readlane(o0_, __builtin_ctzll(__ballot(h0_) | (1ull << 63))); \
+                    node = seld_[0] ? n0_ : node;                                               \
                 }                                                                               \
                 if (nn_ > 0) { /* uniform: clean picks (none for most jobs) */                    \
                 _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) if (s_ < K_ && !seld_[s_]) { \
