@@ -566,7 +566,7 @@ struct CRow {  // node row of a candidate (prefetched)
 #endif
 
 // Multi-node jobs whose fitting dirty rows number k..16 (46 % of C4's placed multi-node jobs): the
-// k smallest dirty keys by compaction into lanes 0..15 (LDS scratch `scr`, 192 B) and rank by
+// k smallest dirty keys by compaction into lanes 0..15 (LDS scratch `scr`, 896 B) and rank by
 // count (each of the ≤ 16 keys broadcast, every lane counts the smaller ones) — no sequential wave
 // minima.  Exact when no clean candidate key is below the k-th dirty key (then the k smallest of
 // all are these; 95 % of the cases): returns true and fills drank / kth, else false (the caller
@@ -582,10 +582,11 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
     const int p0 = (int)__builtin_amdgcn_mbcnt_hi(hi0, __builtin_amdgcn_mbcnt_lo(lo0, 0u));
     const int p1 = __builtin_popcountll(m0) + (int)__builtin_amdgcn_mbcnt_hi(hi1, __builtin_amdgcn_mbcnt_lo(lo1, 0u));
     const bool v0 = dk[0] != KEY_INF, v1 = dk[1] != KEY_INF;
+    // branch-free: a lane without a fitting entry writes to its own trash slot (16 + lane)
     L64 keys = (L64)(uintptr_t)scr;
-    L32 ranks = (L32)(uintptr_t)(scr + 128u);
-    if (v0) keys[p0] = dk[0];
-    if (v1) keys[p1] = dk[1];
+    L32 ranks = (L32)(uintptr_t)(scr + 8u * 80u);
+    keys[v0 ? p0 : 16 + lane] = dk[0];
+    keys[v1 ? p1 : 16 + lane] = dk[1];
     const uint64_t x = lane < nd ? keys[lane & 15] : KEY_INF;  // (one wave: LDS in order)
     int r = 0;
 #pragma unroll
@@ -601,8 +602,9 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
     bool below = false;
     for (int k = 0; k < epl; ++k) below = below || (cc[k] && kc[k] < t);
     if (__ballot(below) != 0ull) return false;  // a clean key among the k smallest
-    if (lane < 16) ranks[lane] = r;
-    const int32_t r0 = v0 ? ranks[p0] : 64, r1 = v1 ? ranks[p1] : 64;
+    ranks[lane] = r;  // (lanes 16..63: unused slots)
+    const int32_t q0 = ranks[v0 ? p0 : 16 + lane], q1 = ranks[v1 ? p1 : 16 + lane];
+    const int32_t r0 = v0 ? q0 : 64, r1 = v1 ? q1 : 64;
     drank[0] = r0 < K ? r0 : -1;
     drank[1] = r1 < K ? r1 : -1;
     kth = t;
