@@ -682,29 +682,32 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
                 got_ = select_k<EPL>(K_, kr[A], cl[A], dk, sel_, seld_, kth_, drank_);          \
             }                                                                                   \
             /* the picks' node rows, lane s holding pick s's: one memory round trip per job */  \
-            uint32_t myp_ = 0u;                                                                 \
-            _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) myp_ =                      \
-                lane == s_ ? (uint32_t)sel_[s_] : myp_;                                         \
             uint32_t cpm_ = 0u; /* the clean picks (the only rows read from memory) */          \
             _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) cpm_ |=                     \
                 (s_ < got_ && !seld_[s_]) ? 1u << s_ : 0u;                                      \
             NodeRec mr_ = {0, 0, 0, 0, 0u, 0, 0, 0};                                            \
-            if ((cpm_ >> lane) & 1u) mr_ = rec[myp_];                                           \
-            STAMP(4);                                                                           \
-            if (B != KEY_INF && kth_ > B) {                                                     \
-                stop = 1;                                                                       \
-                goto done;                                                                      \
+            if (cpm_ != 0u) { /* uniform: most jobs pick dirty rows only */                      \
+                uint32_t myp_ = 0u;                                                             \
+                _Pragma("unroll") for (int s_ = 0; s_ < FIT_KMAX; ++s_) myp_ =                  \
+                    lane == s_ ? (uint32_t)sel_[s_] : myp_;                                     \
+                if ((cpm_ >> lane) & 1u) mr_ = rec[myp_];                                       \
             }                                                                                   \
-            if (got_ == K_) {                                                                   \
-                int nn_ = 0;                                                                    \
-                int32_t pnd_ = -1;                                                              \
-                _Pragma("unroll") for (int i = 0; i < FIT_KMAX; ++i) nn_ += i < K_ && !seld_[i]; \
-                STAMP_CNT((unsigned long long)(K_ - nn_));                                      \
-                STAMP_DIRTY_BELOW(A);                                                           \
-                if (nu + nn_ > UCAP) {                                                          \
-                    stop = 2;                                                                   \
+            STAMP(4);                                                                           \
+            int nn_ = 0;                                                                        \
+            _Pragma("unroll") for (int i = 0; i < FIT_KMAX; ++i) nn_ += i < K_ && !seld_[i];    \
+            /* one uniform branch on the common path: a stop (a node outside the lists could  \
+               win; the dirty set is full) or fewer than k nodes (unplaced) are the rare cases */ \
+            const bool st1_ = B != KEY_INF && kth_ > B;                                         \
+            const bool st2_ = got_ == K_ && nu + nn_ > UCAP;                                    \
+            if (st1_ | st2_ | (got_ != K_)) {                                                   \
+                if (st1_ | st2_) {                                                              \
+                    stop = st1_ ? 1 : 2;                                                        \
                     goto done;                                                                  \
                 }                                                                               \
+            } else {                                                                            \
+                int32_t pnd_ = -1;                                                              \
+                STAMP_CNT((unsigned long long)(K_ - nn_));                                      \
+                STAMP_DIRTY_BELOW(A);                                                           \
                 /* the dirty-row picks (89 % at C4) all at once, branch-free: each lane updates \
                    its picked entries (an entry past nu is never picked: its key is INF) and    \
                    stores their node ids at their pick index; the other lanes store to the       \
@@ -812,10 +815,8 @@ __device__ __forceinline__ bool dirty_topk(int K, int nd, uint64_t m0, uint64_t 
         }                                                                                       \
         } /* k == 1 */                                                                          \
         STAMP(5);                                                                               \
-        if (lane == (t & 63)) {                                                                 \
-            oq = jqr[A];                                                                        \
-            ov = node;                                                                          \
-        }                                                                                       \
+        oq = lane == (t & 63) ? jqr[A] : oq; /* (selects: no exec branch) */                    \
+        ov = lane == (t & 63) ? node : ov;                                                      \
         if ((t & 63) == 63) { /* uniform: flush 64 placements */                                \
             if (oq >= 0) out[(int64_t)oq * kmax] = ov;                                          \
             oq = -1;                                                                            \
