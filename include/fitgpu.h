@@ -122,8 +122,16 @@ int fit_nccl_unique_id(void* out128);
  * it waited), and the context stays usable: fit_place restores the node table it started from;
  * fit_place_tl drops the timeline (FIT_E_STATE until fit_load_timeline).  Persistent launches of
  * all contexts on one GPU — in every process — run one at a time (a per-device lock file in
- * FIT_LOCK_DIR, default /tmp; fit_stats.ms_arb_wait). */
+ * fit_lock_dir(); fit_stats.ms_arb_wait). */
 int fit_set_watchdog_us(fit_ctx* ctx, int64_t us);
+/* The directory of the per-GPU lock file that serialises persistent launches across processes:
+ * FIT_LOCK_DIR if set; else /var/run/fitgpu when it is a directory (the hostPath volume every
+ * virtual-kubelet pod of a host mounts: INTEGRATION.md item 6); else /tmp.  Writes it (NUL-
+ * terminated) into buf and returns 0 when the directory is the configured or default shared one,
+ * 1 when it fell back to /tmp — private to one pod in the reference's deployment (one VK pod per
+ * partition, pkg/configurator/configurator.go:188-293), so VKs in other pods on the same GPU are
+ * NOT arbitrated: the caller should warn.  FIT_E_INVAL: buf too small.  No device needed. */
+int fit_lock_dir(char* buf, int32_t buflen);
 
 /* Node table: one row per Slurm node, in Client.Nodes output order (pkg/slurm-agent/slurm.go:
  * 343-364); the row index is the node id placements refer to.  free = total - alloc (the

@@ -49,7 +49,7 @@ hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComp
                         const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
                         const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
                         const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
-                        int32_t* placed);
+                        int32_t* placed, const int32_t* bad);
 hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
                                const int32_t* gpu, const int32_t* av, const uint32_t* mask,
                                const int32_t* perm, int32_t nn, NodeRec* rec);
@@ -213,6 +213,28 @@ struct DevArb {
     std::string path;
 };
 
+// The lock directory.  The lock only serialises launches whose processes see the same file, and
+// the configurator runs every virtual kubelet as its own pod (configurator.go:188-293) with a
+// private /tmp, so the default is a HOST path the VK pod template mounts:
+//   FIT_LOCK_DIR if set (an explicit choice: used as given, a failure to open the file is an error);
+//   else FIT_LOCK_DIR_DEFAULT when it is a directory (the hostPath volume, DirectoryOrCreate);
+//   else /tmp — shared only inside one pod: returned as 1 so the caller can warn (fit_lock_dir).
+constexpr const char* FIT_LOCK_DIR_DEFAULT = "/var/run/fitgpu";
+int resolve_lock_dir(std::string& dir) {
+    const char* e = getenv("FIT_LOCK_DIR");
+    if (e && *e) {
+        dir = e;
+        return 0;
+    }
+    struct stat sb;
+    if (stat(FIT_LOCK_DIR_DEFAULT, &sb) == 0 && S_ISDIR(sb.st_mode)) {
+        dir = FIT_LOCK_DIR_DEFAULT;
+        return 0;
+    }
+    dir = "/tmp";
+    return 1;
+}
+
 DevArb* dev_arb(int device, std::string& err) {
     static std::mutex m;
     static std::map<int, DevArb*> tab;
@@ -224,8 +246,9 @@ DevArb* dev_arb(int device, std::string& err) {
         if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) snprintf(bus, sizeof bus, "dev%d", device);
         for (char* q = bus; *q; ++q)
             if (*q == ':' || *q == '/') *q = '_';
-        const char* dir = getenv("FIT_LOCK_DIR");
-        a->path = std::string(dir && *dir ? dir : "/tmp") + "/fitgpu-" + bus + ".lock";
+        std::string dir;
+        (void)resolve_lock_dir(dir);
+        a->path = dir + "/fitgpu-" + bus + ".lock";
         // every user's engines share the file: created 0666 (fchmod, not the process-wide umask);
         // an existing file of another user in a sticky /tmp may refuse an O_CREAT open
         // (fs.protected_regular), so it is then opened read-only — flock needs no write access
@@ -652,6 +675,10 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     }
     if (c->h_err.p[0]) {
         const int rc = trip_error(c, "placement engine");
+        if (no_backup) {  // no copy was taken: the rows are partly committed, drop the table
+            c->have_nodes = c->have_tl = false;
+            return rc;
+        }
         HIP_TRY(hipMemcpyAsync(c->rec.p, c->rec_bak.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
         return rc;
@@ -728,7 +755,7 @@ int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, 
     for (int k = 0; k <= 32; ++k) sc.nb[k] = c->nb[std::min(k, C)];
     HIP_TRY(hipEventRecord(c->ev[0], st));
     HIP_TRY(launch_small(st, C, c->rec.p, sc, jbd, c->jl.p, cpu, mem, gpu, wall, part, nk, kmax, out,
-                         c->small_placed.p));
+                         c->small_placed.p, g + 1));
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_small.p, g, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
     if (C > 0)
@@ -1271,6 +1298,14 @@ int check_timeline_args(fit_ctx* c, int32_t slots, int32_t slot_min) {
 extern "C" {
 
 int fit_abi_version(void) { return FITGPU_ABI_VERSION; }
+
+int fit_lock_dir(char* buf, int32_t buflen) {
+    std::string dir;
+    const int shared = resolve_lock_dir(dir);
+    if (!buf || buflen <= (int32_t)dir.size()) return fail(FIT_E_INVAL, "fit_lock_dir: buffer too small");
+    memcpy(buf, dir.c_str(), dir.size() + 1);
+    return shared;
+}
 
 const char* fit_strerror(int code) {
     switch (code) {

@@ -16,9 +16,14 @@ constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 job
 constexpr unsigned long long TASK_EXIT = ~0ull;
 
 // ---- watchdog (round 5) ----------------------------------------------------------------------
-// Every wait of the persistent engines is bounded in TIME: `wd` ticks of the 100 MHz realtime
-// counter since the wait began (a kernel argument; fit_set_watchdog_us, default 10 s).  A spin
-// count cannot tell a long legitimate wait (another tenant's kernel holding the CUs) from a hang.
+// The cross-block waits of the persistent engines are bounded in TIME: `wd` ticks of the 100 MHz
+// realtime counter since the wait began (a kernel argument; fit_set_watchdog_us, default 10 s) —
+// the scan workers' ring waits, the committers' round-start waits and k_engine_tl's helpers' tile
+// waits.  A spin count cannot tell a long legitimate wait (another tenant's kernel holding the CUs)
+// from a hang.  k_engine's in-block commit waits (helpers' tile waits, decider <-> helper
+// hand-offs, fit_commit_mw.h) keep a spin bound (MW_SPIN_LIMIT, a few seconds): a clock there
+// costs the VGPR-limited helper +0.55 ms at C3, and what they wait for comes
+// from blocks whose own waits are timed.
 // The first trip of a launch records where it happened (TripRec); fit_last_error reports it.
 __device__ __forceinline__ unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
 // The clock of one wait, free while the wait is short: it is read every 64 spins only (an SMEM

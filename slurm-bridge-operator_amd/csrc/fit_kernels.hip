@@ -297,8 +297,14 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t kmax,
-    int32_t* __restrict__ out, int32_t* __restrict__ placed) {
+    int32_t* __restrict__ out, int32_t* __restrict__ placed, const int32_t* __restrict__ bad) {
     __shared__ uint64_t wmin[SMALL_THREADS / 64];
+    // the job-list kernel (same stream, launched before) flags a job with a negative demand or
+    // nodes_k > kmax; the call then fails with FIT_E_INVAL and must leave the node table as it was
+    if (*bad) {
+        if (threadIdx.x == 0) placed[blockIdx.x] = 0;
+        return;
+    }
     __shared__ int32_t sel[FIT_KMAX];
     const int c = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -360,10 +366,10 @@ hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComp
                         const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
                         const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
                         const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
-                        int32_t* placed) {
+                        int32_t* placed, const int32_t* bad) {
     if (ncomp == 0) return hipSuccess;
     hipLaunchKernelGGL(k_small, dim3(ncomp), dim3(SMALL_THREADS), 0, st, rec, C, jb, jl, jcpu, jmem,
-                       jgpu, jwall, jpart, jk, kmax, out, placed);
+                       jgpu, jwall, jpart, jk, kmax, out, placed, bad);
     return hipGetLastError();
 }
 

@@ -622,15 +622,15 @@ __device__ __forceinline__ int tl_reserve_lds(Seg* L, int n, int cap, int32_t s,
 // Per job, on the fast path, every wait is on LDS or on loads issued one job earlier: the job
 // stream (row, bound, candidate keys) is prefetched with vector loads (in-order vmcnt), and the
 // dirty evaluation, reservation and prefix-minimum update are LDS-only.
-// One component's window, by one wave (host-driven k_commit_tl and the persistent k_engine_tl
-// committers).  smem: commit_tl_lds_bytes() of LDS.
+// One component's window, by one wave (the host-driven k_commit_tl: its window's scan is complete
+// before the launch, so nothing here waits; k_engine_tl commits on the decider / helper split).  smem: commit_tl_lds_bytes() of LDS.
 template <int EPL>
 __device__ __forceinline__ CommitResult commit_tl_window(
     const CompPlan& P, int c, unsigned char* smem, Seg* __restrict__ slab,
     TlHdr* __restrict__ hdr, const uint64_t* __restrict__ cand, int64_t rank_stride, int nranks,
     const uint64_t* __restrict__ bnd, const JobRec* __restrict__ wjob,
     const int32_t* __restrict__ perm, int32_t* __restrict__ out, int32_t* __restrict__ outs,
-    int32_t H, int32_t R, const unsigned* tdone = nullptr, unsigned need = 0) {
+    int32_t H, int32_t R) {
     Seg* scr = reinterpret_cast<Seg*>(smem);                // general-path scratch
     // TL_UCAP regions of R runs, TL_PAD runs apart beyond R: a lane's region starts 16 B further
     // along the banks than its neighbour's, so the lanes' reads of their own lists (the 4-ary
@@ -680,29 +680,8 @@ __device__ __forceinline__ CommitResult commit_tl_window(
 #ifdef FIT_STAMPS
     unsigned long long tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    // tdone (k_engine_tl): the window is committed while its scan tiles run; before a job's row,
-    // bound and candidates are read, its tile must have all `need` slices done; an agent-scope
-    // acquire when a tile turns ready drops this CU's L1 (the buffers are reused every round and
-    // may be cached stale), so the reads themselves stay plain, prefetchable loads
-    int ready = 0;
-    bool tfail = false;
-    auto tile_ready = [&](int tt) {
-        if (!tdone) return true;
-        const int tile = tt / SCAN_JOBS;
-        if (tile < ready) return true;
-        WaitClock clk;
-        for (unsigned sp = 0;; ++sp) {
-            if (__hip_atomic_load(tdone + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-            if (clk.over(sp, 1000000000u)) return false;  // 10 s
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        ready = tile + 1;
-        return true;
-    };
     auto ld64 = [&](const uint64_t* p) { return *p; };
     auto ldjob = [&](const JobRec* p) { return *p; };
-    if (!tile_ready(0)) return CommitResult{0, 3, 0, 0};
     JobRec J = ldjob(wjob + P.slot0 + z);
     uint64_t B = ld64(bnd + P.slot0 + z);
     uint64_t kr[EPL];
@@ -730,10 +709,6 @@ __device__ __forceinline__ CommitResult commit_tl_window(
             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)B);
         {  // the next job's stream, in flight during this one
             const int tn = min(t + 1, P.w - 1);
-            if (!tile_ready(tn)) {
-                tfail = true;
-                break;
-            }
             J = ldjob(wjob + P.slot0 + tn + z);
             B = ld64(bnd + P.slot0 + tn + z);
 #pragma unroll
@@ -983,7 +958,6 @@ __device__ __forceinline__ CommitResult commit_tl_window(
     if (lane == 0)
         for (int i = 0; i < 12; ++i) atomicAdd(&g_tlst[c & 63][i], tacc[i]);
 #endif
-    if (tfail) stop = 3;  // watchdog: a scan tile never completed
     return CommitResult{t, stop, nu, placed};
 }
 

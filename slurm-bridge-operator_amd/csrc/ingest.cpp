@@ -750,17 +750,22 @@ int32_t fit_set_max_array_size(int32_t n) {
     return g_max_array_size.exchange(n);
 }
 
-// Does the script's #SBATCH header (the lines extractBatchResourcesFromScript reads,
-// pkg/slurm-bridge-operator/parse.go:36-46: empty lines and the shebang skipped, the header ends at
-// the first other line) ask for an array (--array[=v] / -a v / -av)?  extractBatchResourcesFromScript
-// ignores it, but sbatch honours it: the pod is then an array job and is never pinned.
+// Does the script ask sbatch for an array (--array[=v] / -a v / -av)?  extractBatchResourcesFromScript
+// ignores it, but sbatch honours it: the pod is then an array job and is never pinned.  sbatch reads
+// #SBATCH directives up to the first line that is neither blank nor a comment, so a plain '#'
+// comment does not end them here (extractBatchResourcesFromScript, pkg/slurm-bridge-operator/
+// parse.go:36-46, stops at the first non-#SBATCH line; for the demand the engine follows it, for
+// this flag it follows sbatch — a missed array would be pinned with --nodelist).
 static bool script_has_array(const char* script) {
     for (const char* p = script; p && *p;) {
         const char* e = strchr(p, '\n');
         const sv line(p, e ? (size_t)(e - p) : strlen(p));
         p = e ? e + 1 : nullptr;
-        if (line.empty() || line.substr(0, 2) == "#!") continue;
-        if (line.substr(0, 7) != "#SBATCH") break;
+        size_t b = 0;
+        while (b < line.size() && isspace((unsigned char)line[b])) ++b;
+        if (b == line.size()) continue;  // blank
+        if (line[b] != '#') break;       // the first command: sbatch reads no further directive
+        if (line.substr(0, 7) != "#SBATCH") continue;  // the shebang, a plain comment
         size_t i = 7;
         while (i < line.size()) {
             while (i < line.size() && isspace((unsigned char)line[i])) ++i;

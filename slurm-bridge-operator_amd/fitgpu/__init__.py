@@ -329,6 +329,15 @@ def node_columns(nodes: list[Node], part_mask: int = 1):
 
 
 # ------------------------------------------------------------------------------- engine
+def lock_dir() -> tuple[str, bool]:
+    """fit_lock_dir: the directory of the per-GPU launch lock file and whether it is the shared
+    one (FIT_LOCK_DIR, or the /var/run/fitgpu host path) rather than the /tmp fallback."""
+    buf = C.create_string_buffer(4096)
+    rc = lib().fit_lock_dir(buf, len(buf))
+    check(rc, "fit_lock_dir")
+    return buf.value.decode(), rc == 0
+
+
 def nccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     check(lib().fit_nccl_unique_id(buf), "fit_nccl_unique_id")

@@ -40,6 +40,7 @@ EXPORTS = [
     "fit_array_tasks", "fit_pod_demand", "fit_script_with_nodelist", "fit_partition_limits",
     "fit_node_columns", "fit_node_names", "fit_admitter_load_table", "fit_admitter_generation",
     "fit_admitter_script", "fit_set_max_array_size", "fit_release_events", "fit_set_watchdog_us",
+    "fit_lock_dir",
 ]
 
 
@@ -139,6 +140,8 @@ def lib() -> C.CDLL:
         L.fit_nccl_unique_id.argtypes = [P]
         if hasattr(L, "fit_set_watchdog_us"):  # (absent from pre-round-5 variant builds, FITGPU_LIB)
             L.fit_set_watchdog_us.argtypes = [P, i64]
+        if hasattr(L, "fit_lock_dir"):  # (absent from pre-round-6 variant builds, FITGPU_LIB)
+            L.fit_lock_dir.argtypes = [C.c_char_p, i32]
         for name in ("fit_load_nodes", "fit_load_nodes_device"):
             getattr(L, name).argtypes = [P, i32, P, P, P, P, P]
         L.fit_load_partitions.argtypes = [P, i32, P, P, P]

@@ -55,6 +55,19 @@ func (e *Engine) SetWatchdog(us int64) error {
 	return check(C.fit_set_watchdog_us(e.ctx, C.int64_t(us)))
 }
 
+// LockDir is the directory of the per-GPU lock file that serialises persistent launches of
+// every engine on a GPU (fit_lock_dir).  shared is false when the library fell back to /tmp: in
+// the configurator's deployment each virtual kubelet is its own pod with a private /tmp, so
+// engines in other pods on the same GPU would not be arbitrated (INTEGRATION.md item 6).
+func LockDir() (dir string, shared bool, err error) {
+	buf := make([]byte, 4096)
+	rc := C.fit_lock_dir((*C.char)(unsafe.Pointer(&buf[0])), C.int32_t(len(buf)))
+	if err := check(rc); err != nil {
+		return "", false, err
+	}
+	return C.GoString((*C.char)(unsafe.Pointer(&buf[0]))), rc == 0, nil
+}
+
 func check(rc C.int) error {
 	if rc < 0 {
 		return &Error{Code: int(rc), Detail: C.GoString(C.fit_last_error())}

@@ -60,6 +60,11 @@ func NewFitAdmission(ctx context.Context, vk *SlurmVirtualKubelet, device int, p
 	if err != nil {
 		return nil, err // no gfx950 device: the caller keeps the reference behaviour
 	}
+	// the device lock must be a host path every VK pod of this host mounts (INTEGRATION.md item 6)
+	if dir, shared, err := fitgpu.LockDir(); err == nil && !shared {
+		klog.Warningf("fit: device lock in %s (no FIT_LOCK_DIR, no /var/run/fitgpu): engines in other "+
+			"virtual-kubelet pods on this GPU are not arbitrated; mount a hostPath at /var/run/fitgpu", dir)
+	}
 	res, err := vk.SlurmClient.Resources(ctx, &workload.ResourcesRequest{Partition: vk.KubeletServer.SlurmPartition})
 	if err != nil {
 		eng.Close()

@@ -37,13 +37,18 @@ ARRAYS = st.one_of(st.none(), st.sampled_from([
 
 
 def script_has_array(script: str) -> bool:
-    """sbatch's --array / -a in the #SBATCH header (the header rule of parse.go:36-46): the pod is
-    an array job (fit_admit_req.flags FIT_REQ_ARRAY), whatever the demand count."""
+    """sbatch's --array / -a among its #SBATCH directives: the pod is an array job
+    (fit_admit_req.flags FIT_REQ_ARRAY), whatever the demand count.  sbatch reads directives up to
+    the first line that is neither blank nor a comment (a plain comment line does not
+    end them, unlike parse.go:36-46's header rule, which the demand itself follows)."""
     for line in script.split("\n"):
-        if line == "" or line.startswith("#!"):
+        body = line.lstrip(" \t\v\f\r")
+        if body == "":
             continue
-        if not line.startswith("#SBATCH"):
+        if not body.startswith("#"):
             break
+        if not line.startswith("#SBATCH"):
+            continue
         if any(t == "--array" or t.startswith("--array=") or t.startswith("-a") for t in line[7:].split()):
             return True
     return False
@@ -77,6 +82,17 @@ def test_pod_demand_matches_oracle(script, nodes, cpt, mpc, tpn, array, ntasks, 
     arr = bool(labels.get("array")) or (script is not None and script_has_array(script))
     for i, g in enumerate(got[:64]):
         assert g == (prio, int(ref[i, 0]), int(ref[i, 1]), 0, int(ref[i, 2]), part, int(ref[i, 3]), int(arr))
+
+
+def test_array_flag_after_a_comment_line():
+    """sbatch keeps reading #SBATCH lines past plain comments, so an --array after
+    one still makes the pod an array job (never pinned); a command line ends the directives."""
+    base = "#!/bin/sh\n#SBATCH --nodes=1\n"
+    flags = lambda sc: [r[7] for r in fitgpu.pod_demand({}, sc)]
+    assert flags(base + "# stage the inputs\n#SBATCH --array=0-3%1\nsrun a\n") == [fitgpu.FIT_REQ_ARRAY]
+    assert flags(base + "\n   \n#SBATCH -a 5\nsrun a\n") == [fitgpu.FIT_REQ_ARRAY]
+    assert flags(base + "srun a\n#SBATCH --array=0-3\n") == [0]
+    assert flags(base + "# only a comment\nsrun a\n") == [0]
 
 
 def test_pod_demand_sample_manifest():

@@ -62,3 +62,37 @@ def test_direct_consecutive_batches(monkeypatch):
         fin = e.read_nodes()
     assert np.array_equal(np.concatenate(got), ref)
     assert all(np.array_equal(a, b) for a, b in zip(fin, rfin))
+
+
+@pytest.mark.parametrize("engine", ["", "direct", "rounds"])
+@pytest.mark.parametrize("bad", ["negative", "kmax"])
+def test_invalid_job_fails_without_consuming(engine, bad, monkeypatch):
+    """a batch of <= 64 jobs with one invalid job (a negative demand, or
+    nodes_k > kmax) fails with FIT_E_INVAL and leaves the node table as it was — k_small checks the
+    job-list kernel's flag before it commits anything, as the rounds path checks it on the host."""
+    import fitgpu
+    from fitgpu import _lib
+    if engine:
+        monkeypatch.setenv("FIT_ENGINE", engine)
+    else:
+        monkeypatch.delenv("FIT_ENGINE", raising=False)
+    nodes, jobs, parts = synth.make_config("c4", 4096, 40)
+    jobs.nodes_k = np.minimum(jobs.nodes_k, 4).astype(np.uint16)
+    if bad == "negative":
+        jobs.cpu[17] = -1
+    else:
+        jobs.nodes_k[17] = 8
+    with Engine(device=0) as e:
+        e.load_partitions(parts)
+        e.load_nodes(nodes)
+        before = e.read_nodes()
+        with pytest.raises(fitgpu.FitError) as ei:
+            e.place(jobs, kmax=4)
+        assert ei.value.code == _lib.FIT_E_INVAL
+        after = e.read_nodes()
+        assert all(np.array_equal(a, b) for a, b in zip(before, after))
+        # the context still places: the valid prefix, bit-exact vs the oracle
+        ok = synth.Jobs(*(x[:17] for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall, jobs.part, jobs.nodes_k)))
+        out, _ = e.place(ok, kmax=4)
+    ref, _, _ = po.ref_place(nodes, ok, parts, kmax=4)
+    assert np.array_equal(out, ref)
