@@ -62,6 +62,21 @@ def kernel_table(agg, stats, steps, world, evals_local, names=("k_scan", "k_comm
     Host-driven rounds (engine == 0): one k_scan + one k_commit launch per round."""
     rounds = max(agg["rounds"], 1)
     jobs_resolved = agg["placed"] + agg["unplaced"]
+    if all(s.get("engine", 0) == 3 for s in stats):
+        # demand-class engine (DESIGN.md §3.10): ONE k_class launch per step, one workgroup per
+        # component; its work is the serial chain (queries of <= 64 set candidates, commits
+        # evaluated against every class, set refills), VALU-issue-bound in one wave per component
+        ms = agg["ms_device"] / steps
+        ops = evals_local / steps * SCAN_OPS_PER_EVAL
+        tops = ops / (ms * 1e-3) / 1e12
+        return {"k_class": {
+            "ms_per_launch": round(ms, 4), "launches": steps, "bound": "valu",
+            "achieved": round(tops, 4), "peak": round(PEAK_VALU_TOPS, 1), "unit": "Tops/s",
+            "frac": round(tops / PEAK_VALU_TOPS, 5),
+            "hbm_gbs_algorithmic": round(evals_local / steps * SCAN_BYTES_PER_EVAL / (ms * 1e-3) / 1e9, 1),
+            "commit_chain_ms": round(agg["ms_commit"] / steps, 3),
+            "commit_ns_per_job": round(agg["ms_commit"] * 1e6 / max(jobs_resolved, 1), 1),
+            "set_refills_longest_component": agg["rounds"] / steps}}
     if all(s.get("engine", 0) == 1 for s in stats):
         ms = agg["ms_device"] / steps
         ops = evals_local / steps * SCAN_OPS_PER_EVAL
@@ -469,9 +484,22 @@ def admission(a):
 
     from fitgpu import Admitter, Engine, synth
     nodes, jobs, parts = synth.make_config("c3")
+    # what ONE virtual kubelet's engine holds (fit_admission.go: one partition per VK,
+    # configurator.go:151-171): partition 0's ~6,250 nodes, its jobs, one partition
+    sel = (nodes.part_mask & 1) != 0
+    n1 = synth.Nodes(*(np.ascontiguousarray(x[sel]) for x in (nodes.cpu_free, nodes.mem_free, nodes.gpu_free,
+                                                               nodes.avail_min)),
+                     np.ones(int(sel.sum()), np.uint32))
+    js = jobs.part == 0
+    j1 = synth.Jobs(*(np.ascontiguousarray(x[js]) for x in (jobs.cpu, jobs.mem, jobs.gpu, jobs.wall)),
+                    np.zeros(int(js.sum()), np.uint16), np.ascontiguousarray(jobs.nodes_k[js]))
+    p1 = synth.Partitions(*(np.ascontiguousarray(x[:1]) for x in (parts.max_time_min, parts.max_cpus_per_node,
+                                                                   parts.max_mem_per_node)))
     callers, per = 10, a.admit_pods
     out = {}
-    for name, mb, mw in (("max_wait_2ms", 1024, 2000), ("max_wait_0", 1024, 0)):
+    for name, mb, mw, (nodes, jobs, parts) in (("max_wait_2ms", 1024, 2000, (nodes, jobs, parts)),
+                                               ("max_wait_0", 1024, 0, (nodes, jobs, parts)),
+                                               ("one_partition_max_wait_0", 1024, 0, (n1, j1, p1))):
         e = Engine(device=0)
         e.load_partitions(parts)
         adm = Admitter(e, max_batch=mb, max_wait_us=mw)
@@ -505,14 +533,39 @@ def admission(a):
         us = np.sort(np.concatenate([np.array(x) for x in lat])) * 1e6
         out[name] = {"pods_per_s": round(callers * per / el, 1), "p50_us": round(float(np.percentile(us, 50)), 1),
                      "p99_us": round(float(np.percentile(us, 99)), 1), "max_us": round(float(us[-1]), 1),
-                     "batches": len(batches), "pods_per_batch": round(callers * per / max(len(batches), 1), 2)}
+                     "batches": len(batches), "pods_per_batch": round(callers * per / max(len(batches), 1), 2),
+                     "nodes": nodes.n, "partitions": parts.p}
+    # where one batch's time goes: fit_place of an admission-sized batch on the
+    # same tables, host wall time of the call (ms_total) against the kernel time on the engine's
+    # stream (ms_device: k_small, HIP events); the rest is the H2D copies of the job columns, the
+    # prefilter + job-list launches, the launch of k_small and the one stream synchronisation
+    split = {}
+    for tname, (tn, tj, tp) in (("c3_table", synth.make_config("c3")), ("one_partition", (n1, j1, p1))):
+        e = Engine(device=0)
+        e.load_partitions(tp)
+        rows = {}
+        for bs in (1, 4, 10, 64):
+            tot, dev = [], []
+            for rep in range(60):
+                e.load_nodes(tn)
+                sub = synth.Jobs(*(np.ascontiguousarray(x[rep * bs:(rep + 1) * bs])
+                                   for x in (tj.cpu, tj.mem, tj.gpu, tj.wall, tj.part, tj.nodes_k)))
+                _, st = e.place(sub)
+                if rep >= 10:
+                    tot.append(st["ms_total"])  # the library's own clock around fit_place
+                    dev.append(st["ms_device"])
+            rows[str(bs)] = {"engine": st["engine"], "call_us_p50": round(1e3 * float(np.median(tot)), 1),
+                             "kernel_us_p50": round(1e3 * float(np.median(dev)), 1),
+                             "host_copies_launch_sync_us_p50": round(1e3 * float(np.median(np.array(tot) - np.array(dev))), 1)}
+        e.close()
+        split[tname] = rows
     best = out["max_wait_0"]
     line = {"metric": "CreatePod admission: pods/s and per-pod latency, 10 concurrent callers, 100k-node table",
             "value": best["pods_per_s"], "unit": "pods/s", "n_gpus": 1, "higher_is_better": True,
             "dtype": "int32", "data": "synthetic c3 node table and job stream (fitgpu/synth.py)",
             "config": {"workload": "admit", "nodes": nodes.n, "callers": callers, "pods": callers * per,
                        "partitions": parts.p},
-            "policies": out,
+            "policies": out, "batch_split": split,
             "reference": "one SubmitJob per CreatePod on 10 PodSyncWorkers, no capacity check "
                          "(provider.go:35-60, options/options.go:107)"}
     print(json.dumps(line), flush=True)

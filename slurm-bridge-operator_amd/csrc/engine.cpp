@@ -7,6 +7,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <hip/hip_vector_types.h>
 #include <rccl/rccl.h>
 #include <sys/file.h>
 #include <sys/stat.h>
@@ -56,6 +57,20 @@ hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t
 hipError_t launch_scatter_nodes(hipStream_t st, const NodeRec* rec, int32_t nn, int32_t* cpu,
                                 int32_t* mem, int32_t* gpu);
 size_t engine_lds_bytes(int32_t max_component_nodes);
+// demand-class engine (fit_class.hip)
+size_t class_lds_bytes(int32_t max_component_nodes);
+int class_max();
+int class_table_slots();
+size_t class_slot_bytes();
+int class_max_nodes();
+hipError_t launch_classify(hipStream_t st, const int8_t* jcomp, const int32_t* jcpu, const int32_t* jmem,
+                           const int32_t* jgpu, const uint16_t* jpart, int32_t nj, void* tab, int4* dem,
+                           int32_t* ncls, int16_t* jcls);
+hipError_t launch_class(hipStream_t st, int ncomp, size_t lds, NodeRec* rec, const int32_t* nbv, uint32_t owned,
+                        const int32_t* jb, const int32_t* jl, const int32_t* jwall, const uint16_t* jk,
+                        const int16_t* jcls, const int4* dem, const int32_t* ncls, int32_t kmax, int32_t* out,
+                        CompOut* co, unsigned* err);
+hipError_t launch_class_out(hipStream_t st, int32_t* out, int64_t n, const NodeRec* rec);
 size_t engine_ctl_bytes();
 size_t engine_ctl_error_offset();
 size_t engine_ctl_trip_offset();
@@ -311,6 +326,19 @@ struct fit_ctx {
     // placements of at most this many jobs run k_small: one launch, the jobs one at a time against
     // every node of their component, no rounds and one host synchronisation (FIT_SMALL_DIRECT)
     int32_t small_direct = 64;
+    // the demand-class engine (fit_class.hip): 0 off (FIT_CLASS=0, FIT_ENGINE=persistent|rounds|
+    // direct), 1 for placements the persistent engine would run, 2 at every size (FIT_ENGINE=class);
+    // used when every component is one partition, fits LDS and has <= class_max() demand classes
+    int cls_mode = 1;
+    bool cls_nodes_ok = false;       // node table: single-partition components that fit LDS
+    int32_t cls_maxn = 0;            // largest component (nodes)
+    DBuf<int16_t> jcls;
+    DBuf<uint8_t> cls_tab;
+    DBuf<int4> cls_dem;
+    DBuf<int32_t> cls_n;
+    DBuf<unsigned> cls_err;
+    HBuf<int32_t> h_cls_n;
+    HBuf<unsigned> h_cls_err;
     DBuf<int32_t> small_placed;
     HBuf<int32_t> h_small;
     int cus = 256;
@@ -401,6 +429,13 @@ struct fit_ctx {
         h_res.release();
         jls.release();
         h_jls.release();
+        jcls.release();
+        cls_tab.release();
+        cls_dem.release();
+        cls_n.release();
+        cls_err.release();
+        h_cls_n.release();
+        h_cls_err.release();
         h_x.release();
         xcount.release();
         h_count.release();
@@ -472,6 +507,21 @@ int load_nodes_common(fit_ctx* c, int32_t n) {
         c->nb[k + 1] += c->nb[k];
     }
     c->nn = c->nb[c->ncomp];
+    {  // the class engine: one partition per component (the part test is then always true) and
+       // the component's rows in one workgroup's LDS
+        int parts_of[32] = {0};
+        for (int p = 0; p < 32; ++p)
+            if (c->comp_of_part[p] >= 0) ++parts_of[c->comp_of_part[p]];
+        c->cls_nodes_ok = c->ncomp > 0 && c->ncomp <= 32;
+        c->cls_maxn = 0;
+        for (int k = 0; k < c->ncomp; ++k) {
+            const int32_t nk = c->nb[k + 1] - c->nb[k];
+            c->cls_maxn = std::max(c->cls_maxn, nk);
+            if (parts_of[k] != 1) c->cls_nodes_ok = false;
+        }
+        if (c->cls_maxn > class_max_nodes() || class_lds_bytes(c->cls_maxn) > 160 * 1024)
+            c->cls_nodes_ok = false;
+    }
     std::vector<int32_t> fill(c->nb.begin(), c->nb.end() - 1), perm(std::max(c->nn, 1));
     for (int32_t x = 0; x < n; ++x)
         if (c->h_mask[x]) perm[fill[c->comp_of_part[__builtin_ctz(c->h_mask[x])]]++] = x;
@@ -711,10 +761,66 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     return 0;
 }
 
+// The demand-class engine (fit_class.hip): one workgroup per component, no
+// cross-block waits (so no launch arbitration), then the positions it wrote become node ids.
+int run_class(fit_ctx* c, int32_t J, const std::vector<int32_t>& jb, const std::vector<char>& owned,
+              const int32_t* wall, const uint16_t* nk, int32_t* out, int32_t kmax, fit_stats& S) {
+    const int C = c->ncomp;
+    hipStream_t st = c->st;
+    if (c->eco.ensure(C) || c->h_eco.ensure(C) || c->cls_err.ensure(1) || c->h_cls_err.ensure(1) ||
+        c->rec_bak.ensure(std::max(c->nn, 1)))
+        return FIT_E_OOM;
+    int32_t* jbd = c->jls.p + joblists_scratch_ints(J) + 2;
+    HIP_TRY(hipMemsetAsync(c->cls_err.p, 0, sizeof(unsigned), st));
+    HIP_TRY(hipMemcpyAsync(c->rec_bak.p, c->rec.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
+    const size_t lds = class_lds_bytes(c->cls_maxn);
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    uint32_t own = 0;  // components this rank places (component sharding; all at world 1)
+    for (int k = 0; k < C; ++k)
+        if (owned[k]) own |= 1u << k;
+    HIP_TRY(launch_class(st, C, lds, c->rec.p, c->nb.data(), own, jbd, c->jl.p, wall, nk, c->jcls.p,
+                         c->cls_dem.p, c->cls_n.p, kmax, out, c->eco.p, c->cls_err.p));
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    HIP_TRY(launch_class_out(st, out, (int64_t)J * kmax, c->rec.p));
+    HIP_TRY(hipMemcpyAsync(c->h_eco.p, c->eco.p, sizeof(CompOut) * C, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_cls_err.p, c->cls_err.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_cls_err.p[0]) {
+        HIP_TRY(hipMemcpyAsync(c->rec.p, c->rec_bak.p, sizeof(NodeRec) * c->nn, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return fail(FIT_E_HIP, "class engine: an in-block wait exceeded its bound (error %u)", c->h_cls_err.p[0]);
+    }
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    S.ms_device += ms;
+    double commit_max = 0;
+    for (int k = 0; k < C; ++k) {
+        if (!owned[k]) continue;
+        const CompOut& o = c->h_eco.p[k];
+        if (o.done_jobs != jb[k + 1] - jb[k])
+            return fail(FIT_E_HIP, "component %d resolved %lld of %d jobs", k, (long long)o.done_jobs,
+                        jb[k + 1] - jb[k]);
+        S.placed += o.placed;
+        S.evals += o.evals;
+        S.rounds = std::max<int64_t>(S.rounds, o.rounds);   // set refills (longest component)
+        S.stops_rescan += o.stops_rescan;                   // exact-scan resolutions
+        S.stops_dirty += o.stops_dirty;
+        commit_max = std::max(commit_max, o.t_commit / 1e5);
+    }
+    S.ms_commit += commit_max;
+    S.engine = 3;
+    return 0;
+}
+
 // Per-component job lists in priority order (stable), built on the device from the prefilter's
 // component ids (launch_joblists: counting sort by component); only the component offsets and
 // two counters come back to the host.  jb[k] .. jb[k+1] = component k's list range.
-int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& jb) {
+// With `classify` the demand classes of every component's jobs are counted in the same
+// synchronisation (k_classify, fit_class.hip); *cls_ok says whether every component has at most
+// class_max() of them.
+int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& jb,
+                    const int32_t* cpu = nullptr, const int32_t* mem = nullptr, const int32_t* gpu = nullptr,
+                    const uint16_t* part = nullptr, bool classify = false, bool* cls_ok = nullptr) {
     const int C = c->ncomp;
     hipStream_t st = c->st;
     if (c->jl.ensure(std::max(J, 1)) || c->jpk.ensure(J + 1) ||
@@ -726,8 +832,24 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
     int32_t* mbd = jbd + C + 1;
     HIP_TRY(launch_joblists(st, c->jcomp.p, J, C, c->jls.p, g, jbd, mbd, c->jl.p, c->jpk.p));
     HIP_TRY(hipMemcpyAsync(c->h_jls.p, g, sizeof(int32_t) * (C + 3), hipMemcpyDeviceToHost, st));
+    if (classify) {
+        const size_t ts = (size_t)C * class_table_slots() * class_slot_bytes();
+        if (c->jcls.ensure(std::max(J, 1)) || c->cls_tab.ensure(ts) ||
+            c->cls_dem.ensure((size_t)C * class_max()) || c->cls_n.ensure(C) || c->h_cls_n.ensure(C))
+            return FIT_E_OOM;
+        HIP_TRY(hipMemsetAsync(c->cls_tab.p, 0, ts, st));
+        HIP_TRY(hipMemsetAsync(c->cls_n.p, 0, sizeof(int32_t) * C, st));
+        HIP_TRY(launch_classify(st, c->jcomp.p, cpu, mem, gpu, part, J, c->cls_tab.p, c->cls_dem.p, c->cls_n.p,
+                                c->jcls.p));
+        HIP_TRY(hipMemcpyAsync(c->h_cls_n.p, c->cls_n.p, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
     if (c->h_jls.p[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
+    if (cls_ok) {
+        *cls_ok = classify;
+        for (int k = 0; classify && k < C; ++k)
+            if (c->h_cls_n.p[k] > class_max()) *cls_ok = false;
+    }
     S.rejected = c->h_jls.p[0];
     jb.assign(c->h_jls.p + 2, c->h_jls.p + 2 + C + 1);
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
@@ -799,8 +921,18 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     // 2. per-component job lists in priority order (stable)
     const int C = c->ncomp;
     std::vector<int32_t> jb;
-    int rc0 = build_job_lists(c, J, S, jb);
+    // the demand-class engine needs the class count of every component: counted in the job
+    // lists' synchronisation when the node table qualifies (world > 1: component sharding only —
+    // the node-sharded layout keeps the host-driven rounds)
+    const int pre_mode = !c->collective() ? 0
+                         : (c->shard_mode == FIT_SHARD_AUTO ? (C >= c->world ? FIT_SHARD_COMPONENTS : FIT_SHARD_NODES)
+                                                            : c->shard_mode);
+    const bool try_cls = c->cls_mode > 0 && c->cls_nodes_ok && pre_mode != FIT_SHARD_NODES &&
+                         (c->cls_mode == 2 || J > c->small_batch);
+    bool cls_ok = false;
+    int rc0 = build_job_lists(c, J, S, jb, cpu, mem, gpu, part, try_cls, &cls_ok);
     if (rc0) return rc0;
+    const bool use_cls = cls_ok && (c->cls_mode == 2 || J - S.rejected > c->small_batch);
 
     // world > 1: split by components (each rank owns whole components, no per-round exchange)
     // or by nodes (north_star: every rank scans 1/world of every component, RCCL each round)
@@ -833,7 +965,10 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     // exchanges candidates over RCCL every round, so it keeps the host loop; a small batch is
     // cheaper as a round or two of k_scan / k_commit than as a whole-chip persistent grid)
     const bool small = J - S.rejected <= c->small_batch;
-    if (c->persistent && !node_sharded && !small) {
+    if (use_cls) {
+        int rc = run_class(c, J, jb, owned, wall, nk, out, kmax, S);
+        if (rc) return rc;
+    } else if (c->persistent && !node_sharded && !small) {
         int rc = run_persistent(c, jb, owned, cpu, mem, gpu, wall, part, nk, out, kmax, S);
         if (rc) return rc;
         S.engine = 1;
@@ -1366,10 +1501,12 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (const char* ev = getenv("FIT_SMALL_BATCH")) c->small_batch = atoi(ev);
     if (const char* ev = getenv("FIT_SMALL_DIRECT")) c->small_direct = atoi(ev);
     // FIT_ENGINE forces one engine at every size: "rounds", "persistent" or "direct" (k_small)
+    if (const char* ev = getenv("FIT_CLASS")) c->cls_mode = atoi(ev) ? 1 : 0;
     if (const char* ev = getenv("FIT_ENGINE")) {
         c->persistent = strcmp(ev, "rounds") != 0;
-        if (strcmp(ev, "persistent") == 0) c->small_batch = -1;
+        if (strcmp(ev, "persistent") == 0 || strcmp(ev, "class") == 0) c->small_batch = -1;
         c->small_direct = strcmp(ev, "direct") == 0 ? INT32_MAX : -1;
+        c->cls_mode = strcmp(ev, "class") == 0 ? 2 : 0;
     }
     c->rank = o.rank;
     c->world = o.world;
