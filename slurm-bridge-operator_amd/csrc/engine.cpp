@@ -326,10 +326,11 @@ struct fit_ctx {
     // placements of at most this many jobs run k_small: one launch, the jobs one at a time against
     // every node of their component, no rounds and one host synchronisation (FIT_SMALL_DIRECT)
     int32_t small_direct = 64;
-    // the demand-class engine (fit_class.hip): 0 off (FIT_CLASS=0, FIT_ENGINE=persistent|rounds|
-    // direct), 1 for placements the persistent engine would run, 2 at every size (FIT_ENGINE=class);
+    // the demand-class engine (fit_class.hip): 0 off (the default, and FIT_ENGINE=persistent|rounds|
+    // direct), 1 for placements the persistent engine would run (FIT_CLASS=1), 2 at every size
+    // (FIT_ENGINE=class);
     // used when every component is one partition, fits LDS and has <= class_max() demand classes
-    int cls_mode = 1;
+    int cls_mode = 0;
     bool cls_nodes_ok = false;       // node table: single-partition components that fit LDS
     int32_t cls_maxn = 0;            // largest component (nodes)
     DBuf<int16_t> jcls;

@@ -147,21 +147,20 @@ def test_class_fuzz(seed, monkeypatch):
 
 @pytest.mark.auto_engine
 def test_class_is_the_production_choice(monkeypatch):
-    """Unset FIT_ENGINE: a large placement on single-partition components runs the class engine;
-    overlapping partitions (c3o: one component) keep the persistent engine; FIT_CLASS=0 turns it
-    off; a small one stays on the rounds."""
+    """FIT_CLASS=1, FIT_ENGINE unset: a large placement on single-partition components runs the
+    class engine; overlapping partitions (c3o: one component) keep the persistent engine; without
+    FIT_CLASS (the default) the persistent engine runs; a small one stays on the rounds."""
     monkeypatch.delenv("FIT_ENGINE", raising=False)
-    monkeypatch.delenv("FIT_CLASS", raising=False)
+    monkeypatch.setenv("FIT_CLASS", "1")
     nodes, jobs, parts = synth.make_config("c3", 20000, 40000)
     _check(nodes, jobs, parts, engine_id=3)
     nodes, jobs, parts = synth.make_config("c3o", 8000, 40000)
     _check(nodes, jobs, parts, engine_id=1)
-    monkeypatch.setenv("FIT_CLASS", "0")
-    nodes, jobs, parts = synth.make_config("c3", 20000, 40000)
-    _check(nodes, jobs, parts, engine_id=1)
-    monkeypatch.delenv("FIT_CLASS", raising=False)
     nodes, jobs, parts = synth.make_config("c3", 20000, 1500)
     _check(nodes, jobs, parts, engine_id=0)
+    monkeypatch.delenv("FIT_CLASS", raising=False)
+    nodes, jobs, parts = synth.make_config("c3", 20000, 40000)
+    _check(nodes, jobs, parts, engine_id=1)
 
 
 def test_class_consecutive_placements(monkeypatch):
