@@ -109,6 +109,7 @@ struct ClsLds {
     int4 jring[CLS_JR];              // (q, class, wall, k) of the staged jobs
     unsigned long long pool[CLS_POOL];
     uint16_t set[CLS_MAX][CLS_SET];
+    ClsRec sink[64];                 // the decider's lanes 1..63 store here instead of branching
 };
 
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
@@ -474,22 +475,26 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
             return p < n ? p : -1;
         };
         // the job's picks, parked one per lane (lane j = pick j): key and the lane that held it
-        uint32_t pkl = 0, pkh = 0;
+        uint32_t pkl = 0;
         int32_t pkn = -1;
         // query: the k smallest distinct candidate keys; returns how many were found and the k-th
+        int32_t x0 = 0, ln0 = 0;  // the first pick (SGPRs): a k = 1 job parks nothing
         auto extract = [&](uint64_t key, int k, uint64_t& kth) {
-            int np = 0;
-            kth = KEY_INF;
-            for (int j = 0; j < k; ++j) {  // uniform; k = 1 for most jobs
-                int ln = 0;
-                const uint64_t m = wave_min_key_lane(key, ln);
+            int ln = 0;
+            uint64_t m = wave_min_key_lane(key, ln);
+            kth = m;
+            x0 = (int32_t)(uint32_t)m;
+            ln0 = ln;
+            if (m == KEY_INF) return 0;
+            int np = 1;
+            for (int j = 1; j < k; ++j) {  // uniform; multi-node jobs only
+                key = key == m ? KEY_INF : key;
+                m = wave_min_key_lane(key, ln);
                 if (m == KEY_INF) break;
                 pkl = (uint32_t)cls_writelane((int)(uint32_t)m, j, (int)pkl);
-                pkh = (uint32_t)cls_writelane((int)(uint32_t)(m >> 32), j, (int)pkh);
                 pkn = cls_writelane(ln, j, pkn);
                 kth = m;
                 np = j + 1;
-                key = key == m ? KEY_INF : key;
             }
             return np;
         };
@@ -528,7 +533,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
             // then A(t+1) and job t+3's fields, in flight during the extraction
             QA A1 = load_a(has_next ? F1.cl : 0);
             const int4 rj3 = t + 3 < t1j ? ring_at(t + 3) : make_int4(0, 0, 0, 1);
-            if ((t & 15) == 0 && lane == 0) S->ctl.jdone = t;  // ring entries below t are free
+            *(lane == 0 ? &S->ctl.jdone : &S->sink[lane].x) = t;  // ring entries below t are free
             CLS_T(tq2);
             int np;
             uint64_t kth;
@@ -561,12 +566,13 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                     cls_request(S, D, CLS_OP_PICK, (unsigned)F.cl, F.w, (unsigned)F.k);
                     cls_block_op(S, rows, n, tid);
                     np = (int)S->ctl.npick;
-                    for (int j = 0; j < np; ++j) {
-                        const uint64_t m = S->ctl.pick[j];
-                        pkl = (uint32_t)cls_writelane((int)(uint32_t)m, j, (int)pkl);
-                        pkh = (uint32_t)cls_writelane((int)(uint32_t)(m >> 32), j, (int)pkh);
-                        pkn = cls_writelane(-1, j, pkn);
-                    }
+                    // lane j < np: pick j, its row in rq (the commit reads picks' rows by lane)
+                    const uint64_t m = lane < np ? S->ctl.pick[lane < FIT_KMAX ? lane : 0] : 0ull;
+                    pkl = (uint32_t)m;
+                    pkn = lane;
+                    x0 = (int32_t)(uint32_t)S->ctl.pick[0];
+                    ln0 = 0;
+                    rq = rows[lane < np ? (int32_t)(uint32_t)m : 0];
                     ++picks;
                     evals += (int64_t)F.k * n;
                 }
@@ -603,38 +609,24 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                     }
                 }
                 for (int j = 0; j < F.k; ++j) {  // uniform
-                    const int32_t x = __builtin_amdgcn_readlane((int)pkl, j);
-                    const int ln = __builtin_amdgcn_readlane(pkn, j);
+                    const int32_t x = j == 0 ? x0 : __builtin_amdgcn_readlane((int)pkl, j);
+                    const int ln = j == 0 ? ln0 : __builtin_amdgcn_readlane(pkn, j);
+                    // the row the query used (current: each pick is a distinct node)
                     int4 o;
-                    if (ln >= 0) {  // the row the query used (current: each pick is a distinct node)
-                        o.x = __builtin_amdgcn_readlane(rq.x, ln);
-                        o.y = __builtin_amdgcn_readlane(rq.y, ln);
-                        o.z = __builtin_amdgcn_readlane(rq.z, ln);
-                        o.w = __builtin_amdgcn_readlane(rq.w, ln);
-                    } else {
-                        const int4 v = rows[x];
-                        o = make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                                      __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
-                    }
+                    o.x = __builtin_amdgcn_readlane(rq.x, ln);
+                    o.y = __builtin_amdgcn_readlane(rq.y, ln);
+                    o.z = __builtin_amdgcn_readlane(rq.z, ln);
+                    o.w = __builtin_amdgcn_readlane(rq.w, ln);
                     const int4 nw = make_int4(o.x - d.x, o.y - d.y, o.z - d.z, o.w);
-                    if (lane == 0) {
-                        ClsRec R;
-                        R.x = x;
-                        R.oc = o.x;
-                        R.om = o.y;
-                        R.og = o.z;
-                        R.nc = nw.x;
-                        R.nm = nw.y;
-                        R.ng = nw.z;
-                        R.oi = F.q * kmax + j;  // bookkeeper 0 stores the position there
-                        S->rec[D.ncommit & (CLS_REC - 1)] = R;
-                    }
+                    // lane 0 stores the record, the count and the row; lanes 1..63 store into their
+                    // own sink slots (no branch on the chain, no bank conflict)
+                    ClsRec* rp = lane == 0 ? &S->rec[D.ncommit & (CLS_REC - 1)] : &S->sink[lane];
+                    *reinterpret_cast<int4*>(&rp->x) = make_int4(x, o.x, o.y, o.z);
+                    *reinterpret_cast<int4*>(&rp->nc) = make_int4(nw.x, nw.y, nw.z, F.q * kmax + j);
                     CLS_CBAR();  // record, then the count (one wave's LDS operations run in order)
                     ++D.ncommit;
-                    if (lane == 0) {
-                        lds_st(&S->ctl.ncommit, D.ncommit);
-                        rows[x] = nw;
-                    }
+                    *(lane == 0 ? &S->ctl.ncommit : reinterpret_cast<unsigned*>(&S->sink[lane].oc)) = D.ncommit;
+                    *(lane == 0 ? &rows[x] : reinterpret_cast<int4*>(&S->sink[lane].nc)) = nw;
                     const int slot = CLS_SET + (int)((D.ncommit - 1) & (CLS_RING - 1));
                     if (lane == slot) rpos = x;
                     // the next job's candidates: this node's new row, and the ring lane it took
