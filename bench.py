@@ -8,14 +8,16 @@ would hand them over), wall time of fit_load_nodes + fit_place end to end (H2D, 
 D2H of the placements).  That rate is `value`.  The same placement from HBM-resident inputs
 (fit_load_nodes_device + fit_place_device) is reported as `kernel_path_value`.
 
-N > 1 (default --scaling strong; SURVEY §8 e): ONE 100k × 1M placement split over the ranks.
---shard-mode auto (default) gives each rank whole partition components (C3: 16 components, so
-2 per rank at N = 8) run by the persistent engine, then one RCCL merge; --shard-mode nodes splits
+N > 1 (default --scaling weak; SURVEY §8 e): the placement partitions into
+independent units (partition components), so every rank places its own 100k × 1M cluster shard
+(a disjoint slice of the generator's streams) with no collective in the data path; `value` is the
+placements of all ranks ÷ the slowest rank's time.  --scaling strong splits ONE 100k × 1M
+placement over the ranks instead: --shard-mode auto (default) gives each rank whole partition
+components (C3: 16 components, 2 per rank at N = 8), then one RCCL merge; --shard-mode nodes splits
 every component's nodes (north_star's layout: RCCL allgather of the candidate lists + u64
-min-allreduce of the bounds per round, host-driven rounds).  Either way the step is bounded by
-the longest component's serial commit chain, so strong scaling is flat at best.
---scaling weak gives every rank its own 100k × 1M cluster shard instead (no data-path
-collective; aggregate rate); a strong N > 1 run also reports that rate as the extra key
+min-allreduce of the bounds per round, host-driven rounds).  Either way a strong step is bounded
+by the longest component's serial commit chain, so strong scaling is flat (DESIGN.md §3.5 gives
+the predicted curves); a strong N > 1 run also reports the weak rate as the extra key
 `weak_scaling` (--no-weak-extra skips it).
 
     python bench.py [--gpus N --steps K --warmup W] [--workload c3|c3o|c2|c5]
@@ -134,7 +136,7 @@ def parse_args():
                     help="test only: every rank on cuda:0 with gloo (rehearse N>1 on a 1-GPU box)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC summary (tools/gpu_pmc.sh + tools/pmc_json.py) with HBM bytes/launch")
-    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: strong = one 100k x 1M placement split over the ranks (--shard-mode); "
                          "weak = every rank places its own 100k x 1M cluster shard (no data-path collective)")
     ap.add_argument("--no-weak-extra", action="store_true",

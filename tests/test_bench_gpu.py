@@ -78,10 +78,32 @@ def test_bench_two_rank_strong_rehearsal(shard_mode, workload):
         port = s.getsockname()[1]
     d = run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
              "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse",
-             "--shard-mode", shard_mode, "--workload", workload, "--no-device-path", "--repeats", "1"])
+             "--scaling", "strong", "--shard-mode", shard_mode, "--workload", workload, "--no-device-path",
+             "--repeats", "1"])
     jobs = 1_000_000 if workload == "c3" else 65_536
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["jobs"] == jobs
     assert ("component" in d["config"]["parallelism"]) == (shard_mode == "auto")
     w = d["weak_scaling"]
     assert w["scaling"] == "weak" and w["value"] > 0 and w["per_gpu"]["jobs"] == jobs
 
+
+
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_bench_four_rank_rehearsal(scaling):
+    """the driver's first multi-GPU run can be checked against a number — four
+    ranks rehearsed on one GPU (gloo timing collectives; the strong split exchanges through the
+    host).  Weak (the default): four 100k x 1M shards, aggregate; strong: one C3 placement over
+    four ranks (four components each), plus the weak leg.  Predictions: DESIGN.md §3.5."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    args = ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1", "--rehearse",
+            "--repeats", "1", "--no-device-path", "--scaling", scaling]
+    if scaling == "strong":
+        args.append("--no-weak-extra")
+    d = run(args, timeout=400)
+    assert d["n_gpus"] == 4 and d["scaling"] == scaling and d["value"] > 0
+    assert d["config"]["jobs"] == (4_000_000 if scaling == "weak" else 1_000_000)
+    if scaling == "strong":
+        assert "component" in d["config"]["parallelism"]
