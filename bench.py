@@ -499,16 +499,16 @@ def admission(a):
                                                                    parts.max_mem_per_node)))
     callers, per = 10, a.admit_pods
     out = {}
-    for name, mb, mw, (nodes, jobs, parts) in (("max_wait_2ms", 1024, 2000, (nodes, jobs, parts)),
-                                               ("max_wait_0", 1024, 0, (nodes, jobs, parts)),
-                                               ("one_partition_max_wait_0", 1024, 0, (n1, j1, p1))):
+    for name, mb, mw, (pn, pj, pp) in (("max_wait_2ms", 1024, 2000, (nodes, jobs, parts)),
+                                       ("max_wait_0", 1024, 0, (nodes, jobs, parts)),
+                                       ("one_partition_max_wait_0", 1024, 0, (n1, j1, p1))):
         e = Engine(device=0)
-        e.load_partitions(parts)
+        e.load_partitions(pp)
         adm = Admitter(e, max_batch=mb, max_wait_us=mw)
-        adm.load_nodes(nodes)
+        adm.load_nodes(pn)
         for i in range(20):  # warmup (first launches)
-            adm.admit(i, int(jobs.cpu[i]), int(jobs.mem[i]), int(jobs.gpu[i]), int(jobs.wall[i]), int(jobs.part[i]))
-        adm.load_nodes(nodes)
+            adm.admit(i, int(pj.cpu[i]), int(pj.mem[i]), int(pj.gpu[i]), int(pj.wall[i]), int(pj.part[i]))
+        adm.load_nodes(pn)
         lat = [[] for _ in range(callers)]
         batches = set()
         bar = threading.Barrier(callers)
@@ -518,8 +518,8 @@ def admission(a):
             for i in range(per):
                 q = w * per + i
                 t = time.perf_counter()
-                r = adm.admit(q, int(jobs.cpu[q]), int(jobs.mem[q]), int(jobs.gpu[q]), int(jobs.wall[q]),
-                              int(jobs.part[q]))
+                r = adm.admit(q, int(pj.cpu[q]), int(pj.mem[q]), int(pj.gpu[q]), int(pj.wall[q]),
+                              int(pj.part[q]))
                 lat[w].append(time.perf_counter() - t)
                 batches.add(r[1])
 
@@ -536,11 +536,11 @@ def admission(a):
         out[name] = {"pods_per_s": round(callers * per / el, 1), "p50_us": round(float(np.percentile(us, 50)), 1),
                      "p99_us": round(float(np.percentile(us, 99)), 1), "max_us": round(float(us[-1]), 1),
                      "batches": len(batches), "pods_per_batch": round(callers * per / max(len(batches), 1), 2),
-                     "nodes": nodes.n, "partitions": parts.p}
+                     "nodes": pn.n, "partitions": pp.p}
     # where one batch's time goes: fit_place of an admission-sized batch on the
     # same tables, host wall time of the call (ms_total) against the kernel time on the engine's
-    # stream (ms_device: k_small, HIP events); the rest is the H2D copies of the job columns, the
-    # prefilter + job-list launches, the launch of k_small and the one stream synchronisation
+    # stream (ms_device: k_small, HIP events); the rest is the one packed H2D copy of the job
+    # columns, the launch of k_small, the one D2H copy (placements + stats) and the synchronisation
     split = {}
     for tname, (tn, tj, tp) in (("c3_table", synth.make_config("c3")), ("one_partition", (n1, j1, p1))):
         e = Engine(device=0)

@@ -47,10 +47,9 @@ hipError_t launch_joblists(hipStream_t st, const int8_t* jcomp, int32_t nj, int 
                            int32_t* scratch, int32_t* g, int32_t* jb, int32_t* mb, int32_t* jl,
                            int32_t* jpk);
 hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C,
-                        const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
-                        const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
-                        const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
-                        int32_t* placed, const int32_t* bad);
+                        const int32_t* ptab, int32_t np, const int32_t* jcpu, const int32_t* jmem,
+                        const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                        const uint16_t* jk, int32_t nj, int32_t kmax, int32_t* out, int32_t* stat);
 hipError_t launch_gather_nodes(hipStream_t st, const int32_t* cpu, const int32_t* mem,
                                const int32_t* gpu, const int32_t* av, const uint32_t* mask,
                                const int32_t* perm, int32_t nn, NodeRec* rec);
@@ -342,6 +341,8 @@ struct fit_ctx {
     HBuf<unsigned> h_cls_err;
     DBuf<int32_t> small_placed;
     HBuf<int32_t> h_small;
+    DBuf<uint8_t> jpack;    // fit_place's job columns of a small batch, packed: one H2D copy
+    HBuf<uint8_t> h_jpack;
     int cus = 256;
     DBuf<uint8_t> ectl, ering;
     DBuf<CompState> ecs;
@@ -437,6 +438,10 @@ struct fit_ctx {
         cls_err.release();
         h_cls_n.release();
         h_cls_err.release();
+        small_placed.release();
+        h_small.release();
+        jpack.release();
+        h_jpack.release();
         h_x.release();
         xcount.release();
         h_count.release();
@@ -858,37 +863,34 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
 }
 
 // ------------------------------------------------------------------------ placement
-// A small placement in one launch (k_small, fit_kernels.hip) after the prefilter: the device job
-// lists feed it directly, and the stats come back with the placements (h_out, when the caller
-// holds host memory) in ONE synchronisation.
+// A small placement in one launch (k_small, fit_kernels.hip: prefilter, per-component job order
+// and placement in one kernel) and ONE device-to-host copy: with host memory for the placements
+// (h_out) the stats ride at the tail of the out buffer (fit_place sizes it), so placements and
+// stats come back together into pinned memory.
 int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                  const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
                  int32_t* out, int32_t* h_out, fit_stats& S) {
     const int C = c->ncomp;
+    const int G = std::max(C, 1);  // blocks (block 0 also when the table is empty)
     hipStream_t st = c->st;
-    if (c->jl.ensure(std::max(J, 1)) || c->jpk.ensure(J + 1) ||
-        c->jls.ensure(std::max<size_t>(joblists_scratch_ints(J), 1) + 2 * (C + 1) + 2) ||
-        c->small_placed.ensure(std::max(C, 1)) || c->h_small.ensure(C + 2))
-        return FIT_E_OOM;
-    int32_t* g = c->jls.p + joblists_scratch_ints(J);
-    int32_t* jbd = g + 2;
-    int32_t* mbd = jbd + C + 1;
-    HIP_TRY(launch_joblists(st, c->jcomp.p, J, C, c->jls.p, g, jbd, mbd, c->jl.p, c->jpk.p));
+    const size_t rows = (size_t)J * kmax;
+    const size_t nback = (h_out ? rows : 0) + 2 + G;
+    if (c->small_placed.ensure(2 + G) || c->h_small.ensure(nback)) return FIT_E_OOM;
+    int32_t* stat = h_out ? out + rows : c->small_placed.p;
     SmallComps sc;
     for (int k = 0; k <= 32; ++k) sc.nb[k] = c->nb[std::min(k, C)];
     HIP_TRY(hipEventRecord(c->ev[0], st));
-    HIP_TRY(launch_small(st, C, c->rec.p, sc, jbd, c->jl.p, cpu, mem, gpu, wall, part, nk, kmax, out,
-                         c->small_placed.p, g + 1));
+    HIP_TRY(launch_small(st, C, c->rec.p, sc, c->d_ptab.p, c->np, cpu, mem, gpu, wall, part, nk, J, kmax,
+                         out, stat));
     HIP_TRY(hipEventRecord(c->ev[1], st));
-    HIP_TRY(hipMemcpyAsync(c->h_small.p, g, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
-    if (C > 0)
-        HIP_TRY(hipMemcpyAsync(c->h_small.p + 2, c->small_placed.p, sizeof(int32_t) * C,
-                               hipMemcpyDeviceToHost, st));
-    if (h_out) HIP_TRY(hipMemcpyAsync(h_out, out, sizeof(int32_t) * J * kmax, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_small.p, h_out ? out : stat, sizeof(int32_t) * nback, hipMemcpyDeviceToHost,
+                           st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (c->h_small.p[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
-    S.rejected = c->h_small.p[0];
-    for (int k = 0; k < C; ++k) S.placed += c->h_small.p[2 + k];
+    const int32_t* hs = c->h_small.p + (h_out ? rows : 0);
+    if (hs[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
+    if (h_out) memcpy(h_out, c->h_small.p, sizeof(int32_t) * rows);
+    S.rejected = hs[0];
+    for (int k = 0; k < C; ++k) S.placed += hs[2 + k];
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     S.ms_device = S.ms_commit = ms;
@@ -906,10 +908,6 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     memset(&S, 0, sizeof S);
     S.jobs = J;
     hipStream_t st = c->st;
-    // 1. prefilter: out[] init, FIT_REJECTED, component per job
-    if (c->jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
-    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
-                             c->jcomp.p));
     if (J <= c->small_direct && !c->collective()) {  // a few jobs: one launch, one synchronisation
         const int rc = place_direct(c, J, cpu, mem, gpu, wall, part, nk, kmax, out, h_out, S);
         if (rc) return rc;
@@ -919,6 +917,10 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
         if (stats) *stats = S;
         return 0;
     }
+    // 1. prefilter: out[] init, FIT_REJECTED, component per job
+    if (c->jcomp.ensure(std::max(J, 1))) return FIT_E_OOM;
+    HIP_TRY(launch_prefilter(st, cpu, mem, gpu, wall, part, nk, J, kmax, c->d_ptab.p, c->np, out,
+                             c->jcomp.p));
     // 2. per-component job lists in priority order (stable)
     const int C = c->ncomp;
     std::vector<int32_t> jb;
@@ -1643,6 +1645,9 @@ static int check_place_args(fit_ctx* c, int32_t j, const void* a, const void* b,
     return 0;
 }
 
+// fit_place copies a batch of at most this many jobs as one packed transfer
+constexpr int32_t kPackJobs = 16384;
+
 int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
               const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
               int32_t* out, fit_stats* stats) {
@@ -1651,20 +1656,51 @@ int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, con
     HIP_TRY(hipSetDevice(c->device));
     // demands >= 0 and nodes_k <= kmax are checked on the device (k_prefilter): FIT_E_INVAL
     size_t m = std::max(j, 1);
-    if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
-        c->jpart.ensure(m) || c->jk.ensure(m) || c->out.ensure(m * kmax))
-        return FIT_E_OOM;
-    const size_t b = sizeof(int32_t) * j;
-    HIP_TRY(hipMemcpyAsync(c->jcpu.p, cpu, b, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(hipMemcpyAsync(c->jmem.p, mem, b, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(hipMemcpyAsync(c->jgpu.p, gpu, b, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(hipMemcpyAsync(c->jwall.p, wall, b, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(hipMemcpyAsync(c->jpart.p, part, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
-    if (nk)
-        HIP_TRY(hipMemcpyAsync(c->jk.p, nk, sizeof(uint16_t) * j, hipMemcpyHostToDevice, c->st));
+    // the out buffer's tail holds the direct placement's stats (place_direct: one copy back)
+    if (c->out.ensure(m * kmax + 2 + FIT_MAX_PARTITIONS + 1)) return FIT_E_OOM;
+    const int32_t *dcpu, *dmem, *dgpu, *dwall;
+    const uint16_t *dpart, *dk = nullptr;
+    const size_t b = sizeof(int32_t) * j, bh = sizeof(uint16_t) * j;
+    if (j <= kPackJobs) {
+        // a small batch (admission): the columns packed in pinned memory, ONE copy to the device
+        // (the previous call's copy is complete: every fit_place ends with a synchronisation)
+        const size_t bh4 = (bh + 3) & ~(size_t)3;
+        const size_t tot = 4 * b + 2 * bh4;
+        if (c->jpack.ensure(tot) || c->h_jpack.ensure(tot)) return FIT_E_OOM;
+        uint8_t* h = c->h_jpack.p;
+        memcpy(h, cpu, b);
+        memcpy(h + b, mem, b);
+        memcpy(h + 2 * b, gpu, b);
+        memcpy(h + 3 * b, wall, b);
+        memcpy(h + 4 * b, part, bh);
+        if (nk) memcpy(h + 4 * b + bh4, nk, bh);
+        HIP_TRY(hipMemcpyAsync(c->jpack.p, h, nk ? tot : 4 * b + bh4, hipMemcpyHostToDevice, c->st));
+        uint8_t* d = c->jpack.p;
+        dcpu = (const int32_t*)d;
+        dmem = (const int32_t*)(d + b);
+        dgpu = (const int32_t*)(d + 2 * b);
+        dwall = (const int32_t*)(d + 3 * b);
+        dpart = (const uint16_t*)(d + 4 * b);
+        if (nk) dk = (const uint16_t*)(d + 4 * b + bh4);
+    } else {
+        if (c->jcpu.ensure(m) || c->jmem.ensure(m) || c->jgpu.ensure(m) || c->jwall.ensure(m) ||
+            c->jpart.ensure(m) || c->jk.ensure(m))
+            return FIT_E_OOM;
+        HIP_TRY(hipMemcpyAsync(c->jcpu.p, cpu, b, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(c->jmem.p, mem, b, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(c->jgpu.p, gpu, b, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(c->jwall.p, wall, b, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(c->jpart.p, part, bh, hipMemcpyHostToDevice, c->st));
+        if (nk) HIP_TRY(hipMemcpyAsync(c->jk.p, nk, bh, hipMemcpyHostToDevice, c->st));
+        dcpu = c->jcpu.p;
+        dmem = c->jmem.p;
+        dgpu = c->jgpu.p;
+        dwall = c->jwall.p;
+        dpart = c->jpart.p;
+        if (nk) dk = c->jk.p;
+    }
     bool done = false;
-    rc = place_impl(c, j, c->jcpu.p, c->jmem.p, c->jgpu.p, c->jwall.p, c->jpart.p,
-                    nk ? c->jk.p : nullptr, kmax, c->out.p, stats, out, &done);
+    rc = place_impl(c, j, dcpu, dmem, dgpu, dwall, dpart, dk, kmax, c->out.p, stats, out, &done);
     if (rc) return rc;
     if (done) return 0;  // the direct small placement copied the placements back with its stats
     HIP_TRY(hipMemcpyAsync(out, c->out.p, sizeof(int32_t) * j * kmax, hipMemcpyDeviceToHost,

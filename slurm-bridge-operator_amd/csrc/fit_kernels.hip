@@ -50,6 +50,28 @@ __global__ __launch_bounds__(64) void k_commit(
 
 // ------------------------------------------------------------------- prefilter / setup
 // out[] init, component id per job, rejected marks (FIT_REJECTED) — DESIGN.md §3.1.
+// The verdict on job q: -3 invalid job (negative demand or nodes_k > kmax), -2 rejected by its
+// partition's limits, -1 partition without nodes, else its component | 0x40 for a multi-node
+// job.  *rej (the FIT_REJECTED rows) and *k (rows of the job) for the out[] init.
+__device__ __forceinline__ int job_code(int q, const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+                                        const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+                                        const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk,
+                                        int32_t kmax, const int32_t* __restrict__ ptab, int32_t np,
+                                        bool* rej, int* k) {
+    const int p = jpart[q];
+    *k = jk ? max((int)jk[q], 1) : 1;
+    bool r = p >= np;
+    if (!r) {
+        const int mt = ptab[p], mc = ptab[32 + p], mm = ptab[64 + p];
+        r = (mt >= 0 && jwall[q] > mt) || (mc >= 0 && jcpu[q] > mc) || (mm >= 0 && jmem[q] > mm);
+    }
+    *rej = r;
+    int comp = r ? -2 : ptab[96 + p];
+    if (comp >= 0 && *k > 1) comp |= 0x40;
+    if (*k > kmax || jcpu[q] < 0 || jmem[q] < 0 || jwall[q] < 0 || (jgpu && jgpu[q] < 0)) comp = -3;
+    return comp;
+}
+
 __global__ void k_prefilter(const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
                             const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall, const uint16_t* __restrict__ jpart,
                             const uint16_t* __restrict__ jk, int32_t nj, int32_t kmax,
@@ -57,20 +79,9 @@ __global__ void k_prefilter(const int32_t* __restrict__ jcpu, const int32_t* __r
                             int32_t np, int32_t* __restrict__ out, int8_t* __restrict__ jcomp) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nj) return;
-    const int p = jpart[q];
-    const int k = jk ? max((int)jk[q], 1) : 1;
-    bool rej = p >= np;
-    if (!rej) {
-        const int mt = ptab[p], mc = ptab[32 + p], mm = ptab[64 + p];
-        rej = (mt >= 0 && jwall[q] > mt) || (mc >= 0 && jcpu[q] > mc) || (mm >= 0 && jmem[q] > mm);
-    }
-    // -3: invalid job (negative demand or nodes_k > kmax), -2: rejected by partition limits,
-    // -1: partition has no nodes, else component | 0x40 for a multi-node job
-    int8_t comp = rej ? (int8_t)-2 : (int8_t)ptab[96 + p];
-    if (comp >= 0 && k > 1) comp = (int8_t)(comp | 0x40);
-    if (k > kmax || jcpu[q] < 0 || jmem[q] < 0 || jwall[q] < 0 || (jgpu && jgpu[q] < 0))
-        comp = (int8_t)-3;
-    jcomp[q] = comp;
+    bool rej;
+    int k;
+    jcomp[q] = (int8_t)job_code(q, jcpu, jmem, jgpu, jwall, jpart, jk, kmax, ptab, np, &rej, &k);
     for (int i = 0; i < kmax; ++i) out[(int64_t)q * kmax + i] = (rej && i < k) ? -2 : -1;
 }
 
@@ -280,96 +291,164 @@ hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, N
 
 // ------------------------------------------------------------- direct small placement
 // A placement of a few jobs (an admission batch: fit_admitter coalesces the PodSyncWorkers'
-// CreatePod calls, a handful of pods at a time) in ONE launch, no host round trip (DESIGN.md
-// §3.9): block c owns partition component c and walks its jobs (device job list jl[jb[c] ..
-// jb[c+1]), priority order) one at a time, each against every node of the component — SPEC §2
-// directly, no candidate lists, no rounds.  Per job: every thread keeps the minimum key of its
-// strided nodes, a wave DPP minimum then an LDS minimum over the 8 waves gives the block's; a
-// multi-node job takes its k smallest distinct keys by k such extractions (each excludes the keys
-// already taken: keys are unique), all or nothing.  The chosen rows are updated in place in `rec`
-// by the threads that hold the choice; the block barrier makes them visible to the next job's
-// scan (same workgroup).  Cost per job ≈ one pass over the component's rows (L2-resident) and
-// 2 barriers per extraction: a few microseconds, so it is used only for small placements
-// (engine.cpp small_direct) — a large one goes through the rounds.
+// CreatePod calls, a handful of pods at a time) in ONE launch and nothing else — no prefilter,
+// no job-list kernels, no memset.  Every block first runs the prefilter over
+// all jobs (job_code; a few dozen jobs): it initialises the out[] rows of its own jobs (block 0
+// also those of rejected, invalid and nodeless ones) and learns whether any job is invalid, in
+// which case no block touches the node table (the call fails with FIT_E_INVAL).  Then block c
+// walks component c's jobs in priority order (index order, compacted 512 at a time into LDS)
+// one at a time, each against every node of the component — SPEC §2 directly, no candidate
+// lists, no rounds.  Per job: every thread keeps the minimum key of its strided nodes, a wave
+// DPP minimum then an LDS minimum over the 8 waves gives the block's; a multi-node job takes its
+// k smallest distinct keys by k such extractions (each excludes the keys already taken: keys are
+// unique), all or nothing.  The chosen rows are updated in place in `rec` by the threads that
+// hold the choice; the block barrier makes them visible to the next job's scan (same
+// workgroup).  Cost per job ≈ one pass over the component's rows (L2-resident) and 2 barriers
+// per extraction: a few microseconds, so it is used only for small placements (engine.cpp
+// small_direct) — a large one goes through the rounds.
+// stat[0] = rejected jobs, stat[1] = 1 if a job is invalid, stat[2 + c] = jobs placed in c.
 constexpr int SMALL_THREADS = 512;
-__global__ __launch_bounds__(SMALL_THREADS) void k_small(
-    NodeRec* rec, SmallComps C, const int32_t* __restrict__ jb, const int32_t* __restrict__ jl,
-    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
-    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
-    const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t kmax,
-    int32_t* __restrict__ out, int32_t* __restrict__ placed, const int32_t* __restrict__ bad) {
-    __shared__ uint64_t wmin[SMALL_THREADS / 64];
-    // the job-list kernel (same stream, launched before) flags a job with a negative demand or
-    // nodes_k > kmax; the call then fails with FIT_E_INVAL and must leave the node table as it was
-    if (*bad) {
-        if (threadIdx.x == 0) placed[blockIdx.x] = 0;
-        return;
-    }
-    __shared__ int32_t sel[FIT_KMAX];
-    const int c = blockIdx.x;
+
+__device__ __forceinline__ int small_place_job(NodeRec* rec, int nb, int ne, int q,
+                                               const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+                                               const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+                                               const uint16_t* __restrict__ jpart, int k, int32_t kmax,
+                                               int32_t* __restrict__ out, uint64_t* wmin, int32_t* sel) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb = C.nb[c], ne = C.nb[c + 1];
-    const int t0 = jb[c], t1 = jb[c + 1];
-    int32_t np = 0;  // jobs placed by this block (thread 0)
-    for (int t = t0; t < t1; ++t) {
-        const int q = jl[t];
-        JobRec J;
-        J.q = q;
-        J.cpu = jcpu[q];
-        J.mem = jmem[q];
-        J.gpu = jgpu[q];
-        J.wall = jwall[q];
-        J.pbit = 1u << jpart[q];
-        const int k = jk ? max((int)jk[q], 1) : 1;
-        uint64_t prev = 0ull;  // keys <= prev are taken (extraction r excludes them)
-        uint64_t kth = KEY_INF;
-        for (int r = 0; r < k; ++r) {
-            uint64_t m = KEY_INF;
-            for (int p = nb + (int)threadIdx.x; p < ne; p += SMALL_THREADS) {
-                const NodeRec x = rec[p];
-                const uint64_t key = fit_key(x.cpu, x.mem, x.gpu, x.avail, x.mask, (uint32_t)p, J);
-                m = (key < m && (r == 0 || key > prev)) ? key : m;
-            }
-            const uint64_t w = wave_min_key(m);
-            if (lane == 0) wmin[wave] = w;
-            __syncthreads();
-            uint64_t b = wmin[0];
+    JobRec J;
+    J.q = q;
+    J.cpu = jcpu[q];
+    J.mem = jmem[q];
+    J.gpu = jgpu[q];
+    J.wall = jwall[q];
+    J.pbit = 1u << jpart[q];
+    uint64_t prev = 0ull;  // keys <= prev are taken (extraction r excludes them)
+    uint64_t kth = KEY_INF;
+    for (int r = 0; r < k; ++r) {
+        uint64_t m = KEY_INF;
+        for (int p = nb + (int)threadIdx.x; p < ne; p += SMALL_THREADS) {
+            const NodeRec x = rec[p];
+            const uint64_t key = fit_key(x.cpu, x.mem, x.gpu, x.avail, x.mask, (uint32_t)p, J);
+            m = (key < m && (r == 0 || key > prev)) ? key : m;
+        }
+        const uint64_t w = wave_min_key(m);
+        if (lane == 0) wmin[wave] = w;
+        __syncthreads();
+        uint64_t b = wmin[0];
 #pragma unroll
-            for (int i = 1; i < SMALL_THREADS / 64; ++i) b = umin64(b, wmin[i]);
-            __syncthreads();  // wmin is rewritten by the next extraction
-            if (b == KEY_INF) {  // fewer than k nodes fit: nothing is taken
-                kth = KEY_INF;
-                break;
-            }
-            if (m == b) sel[r] = (int32_t)(uint32_t)b;  // the one thread holding it (keys are unique)
-            prev = b;
-            kth = b;
+        for (int i = 1; i < SMALL_THREADS / 64; ++i) b = umin64(b, wmin[i]);
+        __syncthreads();  // wmin is rewritten by the next extraction
+        if (b == KEY_INF) {  // fewer than k nodes fit: nothing is taken
+            kth = KEY_INF;
+            break;
         }
-        __syncthreads();  // sel[]
-        if (kth != KEY_INF) {
-            if ((int)threadIdx.x < k) {
-                const int p = sel[threadIdx.x];
-                const NodeRec x = rec[p];
-                rec[p].cpu = x.cpu - J.cpu;
-                rec[p].mem = x.mem - J.mem;
-                rec[p].gpu = x.gpu - J.gpu;
-                out[(int64_t)q * kmax + threadIdx.x] = x.orig;
-            }
-            ++np;
-        }
-        __syncthreads();  // the updated rows, before the next job's scan
+        if (m == b) sel[r] = (int32_t)(uint32_t)b;  // the one thread holding it (keys are unique)
+        prev = b;
+        kth = b;
     }
-    if (threadIdx.x == 0) placed[c] = np;
+    __syncthreads();  // sel[]
+    if (kth == KEY_INF) return 0;
+    if ((int)threadIdx.x < k) {
+        const int p = sel[threadIdx.x];
+        const NodeRec x = rec[p];
+        rec[p].cpu = x.cpu - J.cpu;
+        rec[p].mem = x.mem - J.mem;
+        rec[p].gpu = x.gpu - J.gpu;
+        out[(int64_t)q * kmax + threadIdx.x] = x.orig;
+    }
+    __syncthreads();  // the updated rows, before the next job's scan
+    return 1;
 }
 
+__global__ __launch_bounds__(SMALL_THREADS) void k_small(
+    NodeRec* rec, SmallComps C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t nj, int32_t kmax,
+    int32_t* __restrict__ out, int32_t* __restrict__ stat) {
+    __shared__ uint64_t wmin[SMALL_THREADS / 64];
+    __shared__ int32_t sel[FIT_KMAX];
+    __shared__ int32_t list[SMALL_THREADS];
+    __shared__ int32_t wcnt[SMALL_THREADS / 64];
+    __shared__ int32_t s_bad, s_rej;
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_bad = s_rej = 0;
+    __syncthreads();
+    // 1. the prefilter, over every job in every block (each needs the invalid-job verdict)
+    int bad = 0, rj = 0;
+    for (int q = threadIdx.x; q < nj; q += SMALL_THREADS) {
+        bool rej;
+        int k;
+        const int code = job_code(q, jcpu, jmem, jgpu, jwall, jpart, jk, kmax, ptab, np, &rej, &k);
+        bad |= code == -3;
+        rj += code == -2;
+        if ((code >= 0 ? (code & 0x3f) : 0) == c)
+            for (int i = 0; i < kmax; ++i) out[(int64_t)q * kmax + i] = (rej && i < k) ? -2 : -1;
+    }
+    if (bad) s_bad = 1;
+    if (rj) atomicAdd(&s_rej, rj);
+    __syncthreads();
+    if (s_bad) {  // the call fails and must leave the node table as it was
+        if (threadIdx.x == 0) {
+            stat[2 + c] = 0;
+            if (c == 0) {
+                stat[0] = s_rej;
+                stat[1] = 1;
+            }
+        }
+        return;
+    }
+    // 2. component c's jobs in priority order
+    int32_t placed = 0;
+    if (c < ncomp) {
+        const int nb = C.nb[c], ne = C.nb[c + 1];
+        for (int base = 0; base < nj; base += SMALL_THREADS) {
+            const int q = base + (int)threadIdx.x;
+            bool mine = false;
+            int k = 1;
+            if (q < nj) {
+                bool rej;
+                const int code = job_code(q, jcpu, jmem, jgpu, jwall, jpart, jk, kmax, ptab, np, &rej, &k);
+                mine = code >= 0 && (code & 0x3f) == c;
+            }
+            const uint64_t m = __ballot(mine);
+            if (lane == 0) wcnt[wave] = __popcll(m);
+            __syncthreads();
+            int off = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < SMALL_THREADS / 64; ++w) {
+                const int n = wcnt[w];
+                off += w < wave ? n : 0;
+                tot += n;
+            }
+            // (q, k) packed: k <= FIT_KMAX
+            if (mine) list[off + __popcll(m & ((1ull << lane) - 1ull))] = q * 32 + k;
+            __syncthreads();
+            for (int t = 0; t < tot; ++t) {
+                const int e = list[t];
+                placed += small_place_job(rec, nb, ne, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31, kmax,
+                                          out, wmin, sel);
+            }
+            __syncthreads();  // list[] and wcnt[] are rewritten by the next chunk
+        }
+    }
+    if (threadIdx.x == 0) {
+        stat[2 + c] = placed;
+        if (c == 0) {
+            stat[0] = s_rej;
+            stat[1] = 0;
+        }
+    }
+}
+
+// grid: max(ncomp, 1) blocks (block 0 initialises the rows of jobs that no component owns)
 hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C,
-                        const int32_t* jb, const int32_t* jl, const int32_t* jcpu,
-                        const int32_t* jmem, const int32_t* jgpu, const int32_t* jwall,
-                        const uint16_t* jpart, const uint16_t* jk, int32_t kmax, int32_t* out,
-                        int32_t* placed, const int32_t* bad) {
-    if (ncomp == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_small, dim3(ncomp), dim3(SMALL_THREADS), 0, st, rec, C, jb, jl, jcpu, jmem,
-                       jgpu, jwall, jpart, jk, kmax, out, placed, bad);
+                        const int32_t* ptab, int32_t np, const int32_t* jcpu, const int32_t* jmem,
+                        const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
+                        const uint16_t* jk, int32_t nj, int32_t kmax, int32_t* out, int32_t* stat) {
+    hipLaunchKernelGGL(k_small, dim3(ncomp > 0 ? ncomp : 1), dim3(SMALL_THREADS), 0, st, rec, C, ncomp, ptab,
+                       np, jcpu, jmem, jgpu, jwall, jpart, jk, nj, kmax, out, stat);
     return hipGetLastError();
 }
 
