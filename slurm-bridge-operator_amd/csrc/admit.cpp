@@ -21,10 +21,14 @@
 // differ (a release, a group that has to be re-placed).  The engine clamps free values at -1
 // (k_gather_nodes), which is exact for placement but cannot be added back to.
 //
-// Threads: callers enqueue under `m` and wait on their own unit's `done` flag (cv `cv_done`);
+// Threads: callers enqueue under `m` and wait on their own unit's `done` flag — spinning for up to
+// kSpinCaller first (a batch takes a few tens of µs; a futex wake-up costs as much again, twice
+// per pod: the coalescer's and the caller's), then on cv `cv_done`; the coalescer likewise spins
+// for up to kSpinCoalescer on the queue after a batch before it blocks;
 // the coalescer thread owns the fit_ctx for the duration of a batch; table loads, queries and the
 // reservation calls take `ctx_m`, so they never interleave with a placement.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -62,7 +66,7 @@ struct Unit {
     int32_t n;
     int64_t seq;      // arrival order (tie-break of equal priorities)
     Clock::time_point t_in;
-    bool done = false;
+    std::atomic<bool> done{false};  // set under `m` (release); callers spin on it without `m`
     int rc = FIT_OK;
     std::string err;  // fit_last_error of the batch, for the caller's thread
 };
@@ -90,6 +94,12 @@ int32_t sat32(int64_t v) { return v > INT32_MAX ? INT32_MAX : v < INT32_MIN ? IN
 
 }  // namespace
 
+// spin budgets before blocking (see the Threads note at the top)
+constexpr std::chrono::microseconds kSpinCaller{200};
+constexpr std::chrono::microseconds kSpinCoalescer{50};
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
 struct fit_admitter {
     fit_ctx* ctx;
     int32_t max_batch;
@@ -99,6 +109,7 @@ struct fit_admitter {
     std::condition_variable cv_work;    // coalescer: a request arrived / stop
     std::condition_variable cv_done;    // callers: a batch finished
     std::deque<Unit*> pending;
+    std::atomic<int32_t> queued{0};     // pending.size(), for the coalescer's spin outside `m`
     int32_t pending_jobs = 0;
     bool stop = false;
     int64_t next_seq = 0;
@@ -284,12 +295,20 @@ void fit_admitter::run() {
     std::vector<Unit*> b;
     std::unique_lock<std::mutex> lk(m);
     for (;;) {
+        if (pending.empty() && !stop) {  // a short spin before blocking: the next pod is likely close
+            lk.unlock();
+            const Clock::time_point until = Clock::now() + kSpinCoalescer;
+            while (queued.load(std::memory_order_relaxed) == 0 && Clock::now() < until) cpu_relax();
+            lk.lock();
+        }
         cv_work.wait(lk, [&] { return stop || !pending.empty(); });
         if (stop) break;
         // the batch stays open max_wait after its first request, or until it is full
-        const Clock::time_point close = pending.front()->t_in + max_wait;
-        cv_work.wait_until(lk, close, [&] { return stop || pending_jobs >= max_batch; });
-        if (stop) break;
+        if (max_wait.count() > 0) {
+            const Clock::time_point close = pending.front()->t_in + max_wait;
+            cv_work.wait_until(lk, close, [&] { return stop || pending_jobs >= max_batch; });
+            if (stop) break;
+        }
         b.clear();
         int32_t jobs = 0;
         // whole units up to max_batch requests (a unit larger than max_batch goes alone)
@@ -298,19 +317,21 @@ void fit_admitter::run() {
             pending_jobs -= pending.front()->n;
             b.push_back(pending.front());
             pending.pop_front();
+            queued.fetch_sub(1, std::memory_order_relaxed);
         }
         lk.unlock();  // new requests queue for the next batch meanwhile
         place_batch(b);
         lk.lock();
-        for (Unit* u : b) u->done = true;
+        for (Unit* u : b) u->done.store(true, std::memory_order_release);
         cv_done.notify_all();
     }
     for (Unit* u : pending) {  // shutting down: nothing more is placed
         u->rc = FIT_E_STATE;
         u->err = "admitter destroyed while the request was queued";
-        u->done = true;
+        u->done.store(true, std::memory_order_release);
     }
     pending.clear();
+    queued.store(0, std::memory_order_relaxed);
     pending_jobs = 0;
     cv_done.notify_all();
 }
@@ -338,9 +359,14 @@ int enqueue_and_wait(fit_admitter* a, const fit_admit_req* reqs, int32_t n, fit_
     u.seq = a->next_seq++;
     ++a->inside;
     a->pending.push_back(&u);
+    a->queued.fetch_add(1, std::memory_order_relaxed);
     a->pending_jobs += n;
     a->cv_work.notify_one();
-    a->cv_done.wait(lk, [&] { return u.done; });
+    lk.unlock();
+    const Clock::time_point until = Clock::now() + kSpinCaller;
+    while (!u.done.load(std::memory_order_acquire) && Clock::now() < until) cpu_relax();
+    lk.lock();
+    a->cv_done.wait(lk, [&] { return u.done.load(std::memory_order_acquire); });
     if (--a->inside == 0 && a->stop) a->cv_done.notify_all();  // destroy may be waiting
     if (u.rc != FIT_OK) fitgpu::set_last_error(u.err.c_str());
     return u.rc;

@@ -360,6 +360,82 @@ __device__ __forceinline__ int small_place_job(NodeRec* rec, int nb, int ne, int
     return 1;
 }
 
+// The same for a component of at most SMALL_THREADS × SMALL_RPT rows, held in VGPRs: thread t
+// owns rows nb + t + 512 i (i < rpt), loaded once per launch with every load in flight, so a job
+// costs ALU and two barriers per extraction instead of a pass over L2 (a pass of dependent loads
+// is ~1 µs of latency per row a thread holds).  The winner of extraction r updates its own
+// registers, writes the row back to `rec` (the table the next call and fit_read_nodes see) and
+// the placement; the next job reads only its own registers, so no trailing barrier is needed.
+constexpr int SMALL_RPT = 16;
+
+__device__ __forceinline__ int small_place_job_regs(NodeRec* rec, int nb, int rpt, int q,
+                                                    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+                                                    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+                                                    const uint16_t* __restrict__ jpart, int k, int32_t kmax,
+                                                    int32_t* __restrict__ out, uint64_t* wmin, int32_t* sel,
+                                                    int32_t (&rc)[SMALL_RPT], int32_t (&rm)[SMALL_RPT],
+                                                    int32_t (&rg)[SMALL_RPT], const int32_t (&ra)[SMALL_RPT],
+                                                    const uint32_t (&rk)[SMALL_RPT], const int32_t (&ro)[SMALL_RPT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    JobRec J;
+    J.q = q;
+    J.cpu = jcpu[q];
+    J.mem = jmem[q];
+    J.gpu = jgpu[q];
+    J.wall = jwall[q];
+    J.pbit = 1u << jpart[q];
+    uint64_t prev = 0ull;
+    uint64_t kth = KEY_INF;
+    uint32_t won = 0;  // extractions this thread won
+    for (int r = 0; r < k; ++r) {
+        uint64_t m = KEY_INF;
+#pragma unroll
+        for (int i = 0; i < SMALL_RPT; ++i) {
+            if (i < rpt) {
+                const uint64_t key = fit_key(rc[i], rm[i], rg[i], ra[i], rk[i],
+                                             (uint32_t)(nb + (int)threadIdx.x + i * SMALL_THREADS), J);
+                m = (key < m && (r == 0 || key > prev)) ? key : m;
+            }
+        }
+        const uint64_t w = wave_min_key(m);
+        if (lane == 0) wmin[wave] = w;
+        __syncthreads();
+        uint64_t b = wmin[0];
+#pragma unroll
+        for (int i = 1; i < SMALL_THREADS / 64; ++i) b = umin64(b, wmin[i]);
+        __syncthreads();  // wmin is rewritten by the next extraction
+        if (b == KEY_INF) {
+            kth = KEY_INF;
+            break;
+        }
+        if (m == b) {
+            sel[r] = (int32_t)(uint32_t)b;
+            won |= 1u << r;
+        }
+        prev = b;
+        kth = b;
+    }
+    if (kth == KEY_INF) return 0;
+    for (int r = 0; won; ++r, won >>= 1) {
+        if (!(won & 1u)) continue;
+        const int p = sel[r];
+        const int ii = (p - nb) / SMALL_THREADS;
+#pragma unroll
+        for (int i = 0; i < SMALL_RPT; ++i) {
+            if (i == ii) {
+                rc[i] -= J.cpu;
+                rm[i] -= J.mem;
+                rg[i] -= J.gpu;
+                rec[p].cpu = rc[i];
+                rec[p].mem = rm[i];
+                rec[p].gpu = rg[i];
+                out[(int64_t)q * kmax + r] = ro[i];
+            }
+        }
+    }
+    return 1;
+}
+
 __global__ __launch_bounds__(SMALL_THREADS) void k_small(
     NodeRec* rec, SmallComps C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
@@ -403,6 +479,26 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
     int32_t placed = 0;
     if (c < ncomp) {
         const int nb = C.nb[c], ne = C.nb[c + 1];
+        // rows in VGPRs when the component fits (SMALL_RPT per thread), else a pass per extraction
+        const int rpt = (ne - nb + SMALL_THREADS - 1) / SMALL_THREADS;
+        const bool regs = rpt <= SMALL_RPT;
+        int32_t rc[SMALL_RPT], rm[SMALL_RPT], rg[SMALL_RPT], ra[SMALL_RPT], ro[SMALL_RPT];
+        uint32_t rk[SMALL_RPT];
+#pragma unroll
+        for (int i = 0; i < SMALL_RPT; ++i) {
+            const int p = nb + (int)threadIdx.x + i * SMALL_THREADS;
+            NodeRec x;
+            x.cpu = x.mem = x.gpu = x.avail = -1;
+            x.mask = 0u;
+            x.orig = -1;
+            if (regs && p < ne) x = rec[p];
+            rc[i] = x.cpu;
+            rm[i] = x.mem;
+            rg[i] = x.gpu;
+            ra[i] = x.avail;
+            rk[i] = x.mask;  // 0: a padding row fits no job
+            ro[i] = x.orig;
+        }
         for (int base = 0; base < nj; base += SMALL_THREADS) {
             const int q = base + (int)threadIdx.x;
             bool mine = false;
@@ -427,8 +523,10 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
             __syncthreads();
             for (int t = 0; t < tot; ++t) {
                 const int e = list[t];
-                placed += small_place_job(rec, nb, ne, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31, kmax,
-                                          out, wmin, sel);
+                placed += regs ? small_place_job_regs(rec, nb, rpt, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31,
+                                                      kmax, out, wmin, sel, rc, rm, rg, ra, rk, ro)
+                               : small_place_job(rec, nb, ne, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31, kmax,
+                                                 out, wmin, sel);
             }
             __syncthreads();  // list[] and wcnt[] are rewritten by the next chunk
         }

@@ -2,7 +2,8 @@
 component) that admission batches run on — bit-exact against the oracle
 (oracle/fitref.c ref_place) at sizes far beyond its production range (FIT_ENGINE=direct forces it
 at every size): the C3 prefix (16 components), one large component (c3o), multi-node jobs up to
-kmax 8 (c4), and the automatic choice at its threshold (FIT_SMALL_DIRECT)."""
+kmax 8 (c4), components past the VGPR-resident size, and the automatic choice at its threshold
+(FIT_SMALL_DIRECT)."""
 import numpy as np
 import pytest
 
@@ -27,8 +28,12 @@ def _check(nodes, jobs, parts, kmax=1, engine_id=2):
     return st
 
 
+# components up to 8,192 rows keep them in VGPRs (SMALL_RPT); c3o 12k and c2 10k are one larger
+# component each: a pass over the rows per extraction
 @pytest.mark.parametrize("name,nn,jj,kmax", [("c3", 20000, 60000, 1), ("c3o", 8192, 20000, 1),
-                                              ("c4", 4096, 20000, 8), ("c2", 512, 8192, 1)])
+                                              ("c4", 4096, 20000, 8), ("c2", 512, 8192, 1),
+                                              ("c3o", 12000, 6000, 1), ("c2", 10000, 5000, 1),
+                                              ("c4", 9000, 3000, 8)])
 def test_direct_matches_oracle(name, nn, jj, kmax, monkeypatch):
     monkeypatch.setenv("FIT_ENGINE", "direct")
     nodes, jobs, parts = synth.make_config(name, nn, jj)
