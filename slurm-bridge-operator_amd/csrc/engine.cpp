@@ -75,6 +75,13 @@ size_t engine_ctl_error_offset();
 size_t engine_ctl_trip_offset();
 size_t engine_ring_bytes();
 size_t engine_ring_tasks();
+int engine_ring_groups();
+// components sharing the fullest task ring (fit_engine_ctl.h: component c goes to ring
+// c % min(groups, nc))
+inline int64_t ring_comps(int nc) {
+    const int g = std::max(1, std::min(engine_ring_groups(), nc));
+    return (nc + g - 1) / g;
+}
 int engine_blocks_per_cu(size_t lds);
 hipError_t launch_engine(int blocks, size_t lds, hipStream_t st, void* ctl, void* ring,
                          const void* cs, void* co, CompPlan* plans, int ncomp, NodeRec* rec,
@@ -683,7 +690,8 @@ int run_persistent(fit_ctx* c, const std::vector<int32_t>& jb, const std::vector
     int32_t max_slices = 1;
     for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
     // (+ one tile: a round's first tile may be scanned as twice the slices, K_T0PAIR)
-    if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices > (int64_t)engine_ring_tasks())
+    if ((int64_t)2 * ring_comps(nc) * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices >
+        (int64_t)engine_ring_tasks())
         return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                     nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);
     size_t lds = engine_lds_bytes(maxnodes);
@@ -1151,7 +1159,7 @@ int run_persistent_tl(fit_ctx* c, const std::vector<int32_t>& jb, const int32_t*
         int32_t max_slices = 1;
         for (int i = 0; i < nc; ++i) max_slices = std::max(max_slices, c->h_ecs.p[i].nslice);
         // (+ one tile: a round's first tile may be scanned as twice the slices, TL_T0PAIR)
-        if ((int64_t)2 * nc * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices >
+        if ((int64_t)2 * ring_comps(nc) * ((wcap + SCAN_JOBS - 1) / SCAN_JOBS + 1) * max_slices >
             (int64_t)engine_ring_tasks())
             return fail(FIT_E_INVAL, "task ring too small: %d components x %lld tiles x %d slices",
                         nc, (long long)((wcap + SCAN_JOBS - 1) / SCAN_JOBS), max_slices);

@@ -12,6 +12,42 @@ namespace fitgpu {
 #define FIT_QCAP_LOG2 18
 #endif
 constexpr unsigned QCAP = 1u << FIT_QCAP_LOG2;  // task ring entries (8-byte {epoch, tile} granules)
+// XCD-aware task rings (round 6; A/B switch, off): FIT_XCD_RINGS 1 gives one
+// ring per group of components, group g = c % G with G = min(8, ncomp), and a scan worker serves
+// only its own XCD's group (HW_REG_XCC_ID % G), so a component's node data is read by the CUs of
+// one XCD and stays in that XCD's L2.  Measured (profiles/r06_xcd_rings_ab.txt): live traffic
+// C5 22.5 -> 12.9 GB and C3 3.6 -> 2.3 GB per launch — the node headers every XCD re-fetched
+// are the re-read — but k_engine_tl +11 % and k_engine +2 %: a round start's burst of tiles gets
+// an eighth of the workers.  Letting idle workers take other groups' published tasks (claim by
+// add: +2 % / +0.4 %, 20.0 GB; by compare-and-swap below the tail, with a shared ring for the
+// round-first tiles: 2.3x slower) gave the traffic back or worse.  0: one ring, a worker claims
+// the next index at once and waits for its slot.  A ring is QRING entries: a 256-B header (tail
+// counter at entry 0, head counter at entry 16, own lines) and QCAP task slots.
+#ifndef FIT_XCD_RINGS
+#define FIT_XCD_RINGS 0
+#endif
+constexpr unsigned QGROUPS = FIT_XCD_RINGS ? 8u : 1u;
+constexpr unsigned QHDR = 32u;              // header entries of a ring
+constexpr unsigned QRING = QHDR + QCAP;     // entries per ring
+__device__ __forceinline__ unsigned ring_groups(int ncomp) {
+    return ncomp < (int)QGROUPS ? (unsigned)max(ncomp, 1) : QGROUPS;
+}
+// the ring of component c's group
+__device__ __forceinline__ unsigned long long* comp_ring(unsigned long long* rings, int c, int ncomp) {
+    return rings + (size_t)((unsigned)c % ring_groups(ncomp)) * QRING;
+}
+// the group of this CU's XCD
+__device__ __forceinline__ unsigned worker_group(int ncomp) {
+#if FIT_XCD_RINGS
+    const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;  // HW_REG_XCC_ID
+    return xcc % ring_groups(ncomp);
+#else
+    (void)ncomp;
+    return 0u;
+#endif
+}
+__device__ __forceinline__ unsigned* ring_tail(unsigned long long* ring) { return reinterpret_cast<unsigned*>(ring); }
+__device__ __forceinline__ unsigned* ring_head(unsigned long long* ring) { return reinterpret_cast<unsigned*>(ring + 16); }
 constexpr int ENGINE_TILES = 128;    // job tiles per window (window <= 8192 jobs)
 constexpr unsigned long long TASK_EXIT = ~0ull;
 
@@ -60,10 +96,7 @@ struct WaitClock {
 };
 
 struct alignas(128) EngineCtl {  // zeroed by a memset before every launch
-    unsigned q_tail;   // tiles reserved by committers
-    unsigned pad0[31];
-    unsigned q_head;   // tiles claimed by workers
-    unsigned pad1[31];
+    unsigned pad0[64];  // (round 5's global ring counters: now in each ring's header)
     unsigned finished;  // components done
     unsigned error;     // 1 = watchdog
     unsigned pad2[30];
@@ -106,8 +139,8 @@ static __device__ __forceinline__ void trip_record(EngineCtl* ctl, unsigned bit,
         r.comp = comp;
         r.round = round;
         r.arg = arg;
-        r.q_head = ld_agent(&ctl->q_head);
-        r.q_tail = ld_agent(&ctl->q_tail);
+        r.q_head = 0u;  // per-group rings: the waiting worker's claimed index is in `arg`
+        r.q_tail = 0u;
         r.pubt = pubt;
         r.tdone = tdone;
         r.need = need;
@@ -162,21 +195,23 @@ __device__ __forceinline__ void engine_round_finished(EngineCtl* ctl, int c, uns
 }
 
 // Publish job tiles [from, upto) of component c's window (every block-slice of each) to the task
-// ring: one wave, uniform arguments.  The caller has released (agent scope) what the tasks'
-// scans read — the round's plan, bound / tile-counter resets and node state.
+// ring of c's group (`ring`: comp_ring): one wave, uniform arguments.  The caller has released
+// (agent scope) what the tasks' scans read — the round's plan, bound / tile-counter resets and
+// node state.
 __device__ __forceinline__ void engine_publish(EngineCtl* ctl, unsigned long long* ring,
                                                unsigned from, unsigned upto, unsigned nslice,
                                                unsigned round, unsigned c) {
+    (void)ctl;
     const unsigned lane = threadIdx.x & 63u;
     const unsigned n = (upto - from) * nslice;
     unsigned base = 0;
     if (lane == 0)
-        base = __hip_atomic_fetch_add(&ctl->q_tail, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base = __hip_atomic_fetch_add(ring_tail(ring), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
     for (unsigned i = lane; i < n; i += 64) {
         const unsigned idx = base + i;
         const unsigned tile = from + i / nslice, sl = i % nslice;
-        __hip_atomic_store(ring + (idx & (QCAP - 1)), engine_task(idx / QCAP + 1, round, tile, sl, c),
+        __hip_atomic_store(ring + QHDR + (idx & (QCAP - 1)), engine_task(idx / QCAP + 1, round, tile, sl, c),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -207,6 +242,40 @@ __device__ __forceinline__ void release_agent() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ROCm 7.2 can drop the fence's own wait
+}
+
+// The next task of a scan worker (thread 0): claim the next index of its ring (FIT_XCD_RINGS
+// above) and wait for the slot; TASK_EXIT once every component has finished or a block tripped.
+struct TaskClaim {
+    unsigned long long* ring = nullptr;
+    unsigned idx = 0;
+    bool held = false;
+};
+__device__ __forceinline__ unsigned long long next_task(EngineCtl* ctl, unsigned long long* rings, int ncomp,
+                                                        unsigned own, TaskClaim& cl, unsigned wd) {
+    WaitClock clk;
+    for (unsigned spins = 0;; ++spins) {
+        if (!cl.held) {
+            cl.ring = rings + (size_t)own * QRING;
+            cl.idx = __hip_atomic_fetch_add(ring_head(cl.ring), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cl.held = true;
+        }
+        if (cl.held) {
+            const unsigned long long g = __hip_atomic_load(cl.ring + QHDR + (cl.idx & (QCAP - 1)), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            if ((g >> 32) == (unsigned long long)(cl.idx / QCAP + 1)) {
+                cl.held = false;
+                return g;
+            }
+        }
+        if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) return TASK_EXIT;
+        if (FIT_WD_WORKER ? clk.over(spins, wd) : spins > WD_SPINS) {
+            trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, cl.idx, 0u, ld_agent(&ctl->finished),
+                        (unsigned)ncomp, clk.t0);
+            return TASK_EXIT;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
 }
 
 // Spin (wave 0 of a committer) until component c has completed `target` scan tiles of the

@@ -175,11 +175,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 }
 #endif
                 if (pair) {  // tile 0 as 2 x nslice half-slices, then the rest
-                    engine_publish(ctl, ring, 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
-                    if (npub > 1u) engine_publish(ctl, ring, 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                    engine_publish(ctl, comp_ring(ring, c, ncomp), 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
+                    if (npub > 1u) engine_publish(ctl, comp_ring(ring, c, ncomp), 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                     target[par] += (unsigned)S.nslice;  // tile 0's extra tasks
                 } else {
-                    engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                    engine_publish(ctl, comp_ring(ring, c, ncomp), 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 }
                 if (npub == ntj) target[par] += ntiles;  // else: after the commit (M->pubt)
                 if (multi && !fail) fail = !wait_tiles(ctl, c, par, target[par], wd, rnd);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
                 const bool jit = ENGINE_AHEAD > 0 && M->pubt < ntj;  // block-uniform (before the barrier)
                 R = commit_window_mw(P, M, rec, cand, bnd, wjob, out, kmax,
                                      MwTiles{&ctl->tdone[par][c][0], (unsigned)S.nslice,
-                                             jit ? ring : nullptr, ctl, rnd, (unsigned)c, ntj,
+                                             jit ? comp_ring(ring, c, ncomp) : nullptr, ctl, rnd, (unsigned)c, ntj,
                                              &ctl->tfeas[par][c][0]});
                 // every tile published this round (the committer's and the helpers') must be
                 // complete before a later round reuses its buffer set: count them
@@ -269,33 +269,15 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine(
     }
 
     // ====================================================================== scan worker
+    const unsigned wgrp = worker_group(ncomp);  // this XCD's ring group (fit_engine_ctl.h)
+    TaskClaim claim;
     unsigned long long* task_slot =
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * KS * 64);
     int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
     int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
     for (;;) {
         if (threadIdx.x == 0) {
-            const unsigned idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
-            unsigned long long task = TASK_EXIT;
-            WaitClock clk;
-            for (unsigned spins = 0;; ++spins) {
-                const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
-                                                               __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                if ((g >> 32) == want) {
-                    task = g;
-                    break;
-                }
-                if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (FIT_WD_WORKER ? clk.over(spins, wd) : spins > WD_SPINS) {
-                    trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
-                                (unsigned)ncomp, clk.t0);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
+            unsigned long long task = next_task(ctl, ring, ncomp, wgrp, claim, wd);
             if (task != TASK_EXIT && task_dropped(ctl, task)) task |= TASK_SKIP;
             *task_slot = task;
         }
@@ -430,8 +412,9 @@ size_t engine_lds_bytes(int32_t max_component_nodes) {
 size_t engine_ctl_bytes() { return sizeof(EngineCtl); }
 size_t engine_ctl_error_offset() { return offsetof(EngineCtl, error); }
 size_t engine_ctl_trip_offset() { return offsetof(EngineCtl, trip); }
-size_t engine_ring_bytes() { return sizeof(unsigned long long) * QCAP; }
-size_t engine_ring_tasks() { return QCAP; }  // task-ring entries
+size_t engine_ring_bytes() { return sizeof(unsigned long long) * QRING * QGROUPS; }
+size_t engine_ring_tasks() { return QCAP; }  // task slots per ring
+int engine_ring_groups() { return (int)QGROUPS; }  // rings (components c % groups share one)
 
 int engine_blocks_per_cu(size_t lds) {
     int n = 0;

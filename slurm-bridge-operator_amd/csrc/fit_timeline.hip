@@ -1080,10 +1080,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
                 }
 #endif
                 if (P.k0 & 2) {
-                    engine_publish(ctl, ring, 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
-                    if (npub > 1u) engine_publish(ctl, ring, 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                    engine_publish(ctl, comp_ring(ring, c, ncomp), 0u, 1u, 2u * (unsigned)S.nslice, rnd, (unsigned)c);
+                    if (npub > 1u) engine_publish(ctl, comp_ring(ring, c, ncomp), 1u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 } else {
-                    engine_publish(ctl, ring, 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
+                    engine_publish(ctl, comp_ring(ring, c, ncomp), 0u, npub, (unsigned)S.nslice, rnd, (unsigned)c);
                 }
                 if (lane == 0) reinterpret_cast<TmShared*>(smem)->pubt = npub;
                 acquire_agent();  // run lists written back by this block: CU-wide fresh view
@@ -1098,7 +1098,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
             const CommitResult r =
                 commit_tl_window_mw(P, smem, slab, hdr, cand, bnd, wjob, out, outs, H, R,
                                     MwTiles{&ctl->tdone[par][c][0], (unsigned)S.nslice,
-                                            TL_AHEAD > 0 ? ring : nullptr, ctl, rnd, (unsigned)c, ntj,
+                                            TL_AHEAD > 0 ? comp_ring(ring, c, ncomp) : nullptr, ctl, rnd, (unsigned)c, ntj,
                                             nullptr},
                                     glob);
             // every tile published this round (the committer's and the helpers') must be complete
@@ -1150,39 +1150,16 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void k_engine_tl(
     }
 
     // ======================================================================== scan worker
+    const unsigned wgrp = worker_group(ncomp);  // this XCD's ring group (fit_engine_ctl.h)
+    TaskClaim claim;
     uint64_t(*xk)[TL_KS][64] = reinterpret_cast<uint64_t(*)[TL_KS][64]>(smem);
     unsigned long long* task_slot =
         reinterpret_cast<unsigned long long*>(smem + sizeof(uint64_t) * (SCAN_WAVES / 2) * TL_KS * 64);
     int64_t busy = 0;     // realtime ticks (100 MHz) spent scanning
     int64_t scanned = 0;  // (job, node) evaluations of the tiles scanned (dropped ones excluded)
-    unsigned idx = 0;     // thread 0: the task-ring index claimed and not yet served
-    bool held = false;
     for (;;) {
         if (threadIdx.x == 0) {
-            unsigned long long task = TASK_EXIT;
-            if (!held) {
-                idx = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                held = true;
-            }
-            const unsigned long long want = (unsigned long long)(idx / QCAP + 1);
-            WaitClock clk;
-            for (unsigned spins = 0;; ++spins) {
-                const unsigned long long g = __hip_atomic_load(ring + (idx & (QCAP - 1)),
-                                                               __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                if ((g >> 32) == want) {
-                    task = g;
-                    held = false;
-                    break;
-                }
-                if (ld_agent(&ctl->finished) == (unsigned)ncomp || ld_agent(&ctl->error)) break;
-                if (clk.over(spins, wd)) {
-                    trip_record(ctl, 1u, TRIP_WORKER_RING, 0u, 0u, idx, 0u, ld_agent(&ctl->finished),
-                                (unsigned)ncomp, clk.t0);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
+            unsigned long long task = next_task(ctl, ring, ncomp, wgrp, claim, wd);
             if (task != TASK_EXIT && task_dropped(ctl, task)) task |= TASK_SKIP;
             *task_slot = task;
         }
