@@ -331,7 +331,10 @@ struct fit_ctx {
     int32_t small_batch = 2048;
     // placements of at most this many jobs run k_small: one launch, the jobs one at a time against
     // every node of their component, no rounds and one host synchronisation (FIT_SMALL_DIRECT)
-    int32_t small_direct = 64;
+    // 128: where k_small stops beating the host-driven rounds on one VK's one-partition table
+    // (tools/direct_vs_rounds.py, profiles/r06q_direct_vs_rounds.txt: 184 vs 178 µs at 128 jobs;
+    // the 16-component C3 table breaks even near 1,024)
+    int32_t small_direct = 128;
     // the demand-class engine (fit_class.hip): 0 off (the default, and FIT_ENGINE=persistent|rounds|
     // direct), 1 for placements the persistent engine would run (FIT_CLASS=1), 2 at every size
     // (FIT_ENGINE=class);

@@ -40,9 +40,9 @@ def test_direct_matches_oracle(name, nn, jj, kmax, monkeypatch):
     _check(nodes, jobs, parts, kmax)
 
 
-@pytest.mark.parametrize("j,want", [(1, 2), (64, 2), (65, 0)])
+@pytest.mark.parametrize("j,want", [(1, 2), (128, 2), (129, 0)])
 def test_direct_threshold(j, want, monkeypatch):
-    """Unset FIT_ENGINE: up to 64 jobs run k_small (engine 2), more the host-driven rounds (0)."""
+    """Unset FIT_ENGINE: up to 128 jobs run k_small (engine 2), more the host-driven rounds (0)."""
     monkeypatch.delenv("FIT_ENGINE", raising=False)
     nodes, jobs, parts = synth.make_config("c4", 4096, j)
     _check(nodes, jobs, parts, kmax=8, engine_id=want)
@@ -72,9 +72,10 @@ def test_direct_consecutive_batches(monkeypatch):
 @pytest.mark.parametrize("engine", ["", "direct", "rounds"])
 @pytest.mark.parametrize("bad", ["negative", "kmax"])
 def test_invalid_job_fails_without_consuming(engine, bad, monkeypatch):
-    """a batch of <= 64 jobs with one invalid job (a negative demand, or
-    nodes_k > kmax) fails with FIT_E_INVAL and leaves the node table as it was — k_small checks the
-    job-list kernel's flag before it commits anything, as the rounds path checks it on the host."""
+    """a batch of <= 128 jobs with one invalid job (a negative demand, or
+    nodes_k > kmax) fails with FIT_E_INVAL and leaves the node table as it was — every k_small block
+    runs the prefilter over the whole batch before it commits anything, as the rounds path checks
+    the job-list kernel's flag on the host."""
     import fitgpu
     from fitgpu import _lib
     if engine:
