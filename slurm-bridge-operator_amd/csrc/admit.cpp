@@ -22,7 +22,8 @@
 // (k_gather_nodes), which is exact for placement but cannot be added back to.
 //
 // Threads: callers enqueue under `m` and wait on their own unit's `done` flag — spinning for up to
-// kSpinCaller first (a batch takes a few tens of µs; a futex wake-up costs as much again, twice
+// kSpinCaller first (yielding the core after kSpinHot, so ten waiting callers do not starve the
+// coalescer on a busy host) (a batch takes a few tens of µs; a futex wake-up costs as much again, twice
 // per pod: the coalescer's and the caller's), then on cv `cv_done`; the coalescer likewise spins
 // for up to kSpinCoalescer on the queue after a batch before it blocks;
 // the coalescer thread owns the fit_ctx for the duration of a batch; table loads, queries and the
@@ -96,6 +97,7 @@ int32_t sat32(int64_t v) { return v > INT32_MAX ? INT32_MAX : v < INT32_MIN ? IN
 
 // spin budgets before blocking (see the Threads note at the top)
 constexpr std::chrono::microseconds kSpinCaller{200};
+constexpr std::chrono::microseconds kSpinHot{30};  // callers: pause-spin this long, then yield
 constexpr std::chrono::microseconds kSpinCoalescer{50};
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
@@ -363,8 +365,13 @@ int enqueue_and_wait(fit_admitter* a, const fit_admit_req* reqs, int32_t n, fit_
     a->pending_jobs += n;
     a->cv_work.notify_one();
     lk.unlock();
-    const Clock::time_point until = Clock::now() + kSpinCaller;
-    while (!u.done.load(std::memory_order_acquire) && Clock::now() < until) cpu_relax();
+    const Clock::time_point t0 = Clock::now(), until = t0 + kSpinCaller, hot = t0 + kSpinHot;
+    while (!u.done.load(std::memory_order_acquire)) {
+        const Clock::time_point now = Clock::now();
+        if (now >= until) break;
+        if (now < hot) cpu_relax();
+        else std::this_thread::yield();  // past the hot phase: leave the core to the coalescer
+    }
     lk.lock();
     a->cv_done.wait(lk, [&] { return u.done.load(std::memory_order_acquire); });
     if (--a->inside == 0 && a->stop) a->cv_done.notify_all();  // destroy may be waiting
