@@ -1,5 +1,6 @@
 """One-off wide fuzz sweep (not part of the suite): tests/test_fuzz_gpu.py's random cases for seeds
-[lo, hi), each placed by every engine (persistent, rounds, direct) and compared bit-exactly with
+[lo, hi), each placed by every engine (persistent, rounds, direct, class — the class engine where the table
+qualifies, else its fallback) and compared bit-exactly with
 the oracle (placements, final node state, counters); and the backfill cases of the same seeds
 (persistent and rounds engines: nodes, start slots, final timelines, counters).  Prints one line per 50 seeds and a summary;
 exits non-zero at the first mismatch, naming seed and engine.
@@ -26,7 +27,7 @@ def main(lo: int, hi: int) -> int:
     for seed in range(lo, hi):
         nodes, jobs, parts, kmax = random_case(seed)
         ref, rst, rfin = po.ref_place(nodes, jobs, parts, kmax=kmax)
-        for eng in ("persistent", "rounds", "direct"):
+        for eng in ("persistent", "rounds", "direct", "class"):
             os.environ["FIT_ENGINE"] = eng
             with Engine() as e:
                 e.load_nodes(nodes)
@@ -62,7 +63,7 @@ def main(lo: int, hi: int) -> int:
         multi += int((np.asarray(jobs.nodes_k) > 1).sum())
         if (seed - lo + 1) % 50 == 0:
             print(f"seeds {lo}..{seed}: ok ({cases} placements, {time.time() - t0:.0f} s)", flush=True)
-    print(f"all ok: {hi - lo} seeds x (3 placement + 2 backfill engines) = {cases} runs, {jobs_total} jobs "
+    print(f"all ok: {hi - lo} seeds x (4 placement + 2 backfill engines) = {cases} runs, {jobs_total} jobs "
           f"({multi} multi-node), {time.time() - t0:.0f} s", flush=True)
     return 0
 
