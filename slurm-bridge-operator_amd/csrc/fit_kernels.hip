@@ -309,19 +309,11 @@ hipError_t launch_commit(int ncomp, int epl, size_t lds_bytes, hipStream_t st, N
 // stat[0] = rejected jobs, stat[1] = 1 if a job is invalid, stat[2 + c] = jobs placed in c.
 constexpr int SMALL_THREADS = 512;
 
-__device__ __forceinline__ int small_place_job(NodeRec* rec, int nb, int ne, int q,
-                                               const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
-                                               const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
-                                               const uint16_t* __restrict__ jpart, int k, int32_t kmax,
-                                               int32_t* __restrict__ out, uint64_t* wmin, int32_t* sel) {
+__device__ __forceinline__ int small_place_job(NodeRec* rec, int nb, int ne, const JobRec& J, int k,
+                                               int32_t kmax, int32_t* __restrict__ out, uint64_t* wmin,
+                                               int32_t* sel) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    JobRec J;
-    J.q = q;
-    J.cpu = jcpu[q];
-    J.mem = jmem[q];
-    J.gpu = jgpu[q];
-    J.wall = jwall[q];
-    J.pbit = 1u << jpart[q];
+    const int q = J.q;
     uint64_t prev = 0ull;  // keys <= prev are taken (extraction r excludes them)
     uint64_t kth = KEY_INF;
     for (int r = 0; r < k; ++r) {
@@ -368,22 +360,14 @@ __device__ __forceinline__ int small_place_job(NodeRec* rec, int nb, int ne, int
 // the placement; the next job reads only its own registers, so no trailing barrier is needed.
 constexpr int SMALL_RPT = 16;
 
-__device__ __forceinline__ int small_place_job_regs(NodeRec* rec, int nb, int rpt, int q,
-                                                    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
-                                                    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
-                                                    const uint16_t* __restrict__ jpart, int k, int32_t kmax,
-                                                    int32_t* __restrict__ out, uint64_t* wmin, int32_t* sel,
+__device__ __forceinline__ int small_place_job_regs(NodeRec* rec, int nb, int rpt, const JobRec& J, int k,
+                                                    int32_t kmax, int32_t* __restrict__ out, uint64_t* wmin,
+                                                    int32_t* sel,
                                                     int32_t (&rc)[SMALL_RPT], int32_t (&rm)[SMALL_RPT],
                                                     int32_t (&rg)[SMALL_RPT], const int32_t (&ra)[SMALL_RPT],
                                                     const uint32_t (&rk)[SMALL_RPT], const int32_t (&ro)[SMALL_RPT]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    JobRec J;
-    J.q = q;
-    J.cpu = jcpu[q];
-    J.mem = jmem[q];
-    J.gpu = jgpu[q];
-    J.wall = jwall[q];
-    J.pbit = 1u << jpart[q];
+    const int q = J.q;
     uint64_t prev = 0ull;
     uint64_t kth = KEY_INF;
     uint32_t won = 0;  // extractions this thread won
@@ -444,7 +428,9 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
     int32_t* __restrict__ out, int32_t* __restrict__ stat) {
     __shared__ uint64_t wmin[SMALL_THREADS / 64];
     __shared__ int32_t sel[FIT_KMAX];
-    __shared__ int32_t list[SMALL_THREADS];
+    __shared__ int32_t list[SMALL_THREADS];   // (job, k) of the chunk's own jobs in priority order
+    __shared__ int4 ljob[SMALL_THREADS];      // their (cpu, mem, gpu, wall): read from LDS per job
+    __shared__ int32_t lpart[SMALL_THREADS];
     __shared__ int32_t wcnt[SMALL_THREADS / 64];
     __shared__ int32_t s_bad, s_rej;
     const int c = blockIdx.x;
@@ -518,15 +504,28 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
                 off += w < wave ? n : 0;
                 tot += n;
             }
-            // (q, k) packed: k <= FIT_KMAX
-            if (mine) list[off + __popcll(m & ((1ull << lane) - 1ull))] = q * 32 + k;
+            // (q, k) packed: k <= FIT_KMAX; the job's columns beside it (this thread loaded them
+            // for job_code: no global read per job in the walk)
+            if (mine) {
+                const int at = off + __popcll(m & ((1ull << lane) - 1ull));
+                list[at] = q * 32 + k;
+                ljob[at] = make_int4(jcpu[q], jmem[q], jgpu[q], jwall[q]);
+                lpart[at] = jpart[q];
+            }
             __syncthreads();
             for (int t = 0; t < tot; ++t) {
                 const int e = list[t];
-                placed += regs ? small_place_job_regs(rec, nb, rpt, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31,
-                                                      kmax, out, wmin, sel, rc, rm, rg, ra, rk, ro)
-                               : small_place_job(rec, nb, ne, e >> 5, jcpu, jmem, jgpu, jwall, jpart, e & 31, kmax,
-                                                 out, wmin, sel);
+                const int4 f = ljob[t];
+                JobRec J;
+                J.q = e >> 5;
+                J.cpu = f.x;
+                J.mem = f.y;
+                J.gpu = f.z;
+                J.wall = f.w;
+                J.pbit = 1u << lpart[t];
+                placed += regs ? small_place_job_regs(rec, nb, rpt, J, e & 31, kmax, out, wmin, sel, rc, rm, rg, ra,
+                                                      rk, ro)
+                               : small_place_job(rec, nb, ne, J, e & 31, kmax, out, wmin, sel);
             }
             __syncthreads();  // list[] and wcnt[] are rewritten by the next chunk
         }
