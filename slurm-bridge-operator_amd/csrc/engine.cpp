@@ -46,6 +46,9 @@ size_t joblists_scratch_ints(int32_t nj);
 hipError_t launch_joblists(hipStream_t st, const int8_t* jcomp, int32_t nj, int ncomp,
                            int32_t* scratch, int32_t* g, int32_t* jb, int32_t* mb, int32_t* jl,
                            int32_t* jpk);
+hipError_t launch_small_args(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C, const int32_t* ptab,
+                             int32_t np, const SmallBatch& B, bool has_nk, int32_t nj, int32_t kmax, int32_t* out,
+                             int32_t* stat);
 hipError_t launch_small(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C,
                         const int32_t* ptab, int32_t np, const int32_t* jcpu, const int32_t* jmem,
                         const int32_t* jgpu, const int32_t* jwall, const uint16_t* jpart,
@@ -335,6 +338,10 @@ struct fit_ctx {
     // (tools/direct_vs_rounds.py, profiles/r06q_direct_vs_rounds.txt: 184 vs 178 µs at 128 jobs;
     // the 16-component C3 table breaks even near 1,024)
     int32_t small_direct = 128;
+    // a batch of <= SMALL_ARGJ jobs from host memory rides in k_small's kernel arguments (no copy to
+    // the device), and the call spins on the batch's completion event instead of sleeping in a
+    // stream synchronisation (FIT_SMALL_ARGS=0 / FIT_SYNC_SPIN=0: A/B switches)
+    bool small_args = true, sync_spin = true;
     // the demand-class engine (fit_class.hip): 0 off (the default, and FIT_ENGINE=persistent|rounds|
     // direct), 1 for placements the persistent engine would run (FIT_CLASS=1), 2 at every size
     // (FIT_ENGINE=class);
@@ -878,9 +885,23 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
 // and placement in one kernel) and ONE device-to-host copy: with host memory for the placements
 // (h_out) the stats ride at the tail of the out buffer (fit_place sizes it), so placements and
 // stats come back together into pinned memory.
+// Wait for the stream's work up to now: a short spin on an event (a small placement takes tens of
+// µs, the wake-up of a blocking synchronisation costs about as much), then the blocking wait.
+hipError_t sync_small(fit_ctx* c) {
+    if (c->sync_spin) {
+        hipError_t e = hipEventRecord(c->ev[2], c->st);
+        if (e != hipSuccess) return e;
+        const double t0 = now_ms();
+        while ((e = hipEventQuery(c->ev[2])) == hipErrorNotReady && now_ms() - t0 < 2.0) {
+        }
+        if (e != hipErrorNotReady) return e;
+    }
+    return hipStreamSynchronize(c->st);
+}
+
 int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                  const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
-                 int32_t* out, int32_t* h_out, fit_stats& S) {
+                 int32_t* out, int32_t* h_out, fit_stats& S, const SmallBatch* hb = nullptr) {
     const int C = c->ncomp;
     const int G = std::max(C, 1);  // blocks (block 0 also when the table is empty)
     hipStream_t st = c->st;
@@ -891,12 +912,15 @@ int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, 
     SmallComps sc;
     for (int k = 0; k <= 32; ++k) sc.nb[k] = c->nb[std::min(k, C)];
     HIP_TRY(hipEventRecord(c->ev[0], st));
-    HIP_TRY(launch_small(st, C, c->rec.p, sc, c->d_ptab.p, c->np, cpu, mem, gpu, wall, part, nk, J, kmax,
-                         out, stat));
+    if (hb)
+        HIP_TRY(launch_small_args(st, C, c->rec.p, sc, c->d_ptab.p, c->np, *hb, nk != nullptr, J, kmax, out, stat));
+    else
+        HIP_TRY(launch_small(st, C, c->rec.p, sc, c->d_ptab.p, c->np, cpu, mem, gpu, wall, part, nk, J, kmax,
+                             out, stat));
     HIP_TRY(hipEventRecord(c->ev[1], st));
     HIP_TRY(hipMemcpyAsync(c->h_small.p, h_out ? out : stat, sizeof(int32_t) * nback, hipMemcpyDeviceToHost,
                            st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(sync_small(c));
     const int32_t* hs = c->h_small.p + (h_out ? rows : 0);
     if (hs[1]) return fail(FIT_E_INVAL, "a job has a negative demand or nodes_k > kmax");
     if (h_out) memcpy(h_out, c->h_small.p, sizeof(int32_t) * rows);
@@ -913,14 +937,15 @@ int place_direct(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, 
 
 int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
                const int32_t* wall, const uint16_t* part, const uint16_t* nk, int32_t kmax,
-               int32_t* out, fit_stats* stats, int32_t* h_out = nullptr, bool* h_out_done = nullptr) {
+               int32_t* out, fit_stats* stats, int32_t* h_out = nullptr, bool* h_out_done = nullptr,
+               const SmallBatch* hb = nullptr) {
     const double t0 = now_ms();
     fit_stats S;
     memset(&S, 0, sizeof S);
     S.jobs = J;
     hipStream_t st = c->st;
     if (J <= c->small_direct && !c->collective()) {  // a few jobs: one launch, one synchronisation
-        const int rc = place_direct(c, J, cpu, mem, gpu, wall, part, nk, kmax, out, h_out, S);
+        const int rc = place_direct(c, J, cpu, mem, gpu, wall, part, nk, kmax, out, h_out, S, hb);
         if (rc) return rc;
         if (h_out_done) *h_out_done = h_out != nullptr;
         S.unplaced = J - S.placed - S.rejected;
@@ -1514,6 +1539,8 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     // live jobs, the persistent engine above (FIT_SMALL_DIRECT, FIT_SMALL_BATCH)
     if (const char* ev = getenv("FIT_SMALL_BATCH")) c->small_batch = atoi(ev);
     if (const char* ev = getenv("FIT_SMALL_DIRECT")) c->small_direct = atoi(ev);
+    if (const char* ev = getenv("FIT_SMALL_ARGS")) c->small_args = atoi(ev) != 0;
+    if (const char* ev = getenv("FIT_SYNC_SPIN")) c->sync_spin = atoi(ev) != 0;
     // FIT_ENGINE forces one engine at every size: "rounds", "persistent" or "direct" (k_small)
     if (const char* ev = getenv("FIT_CLASS")) c->cls_mode = atoi(ev) ? 1 : 0;
     if (const char* ev = getenv("FIT_ENGINE")) {
@@ -1669,6 +1696,22 @@ int fit_place(fit_ctx* c, int32_t j, const int32_t* cpu, const int32_t* mem, con
     size_t m = std::max(j, 1);
     // the out buffer's tail holds the direct placement's stats (place_direct: one copy back)
     if (c->out.ensure(m * kmax + 2 + FIT_MAX_PARTITIONS + 1)) return FIT_E_OOM;
+    if (c->small_args && j <= SMALL_ARGJ && j <= c->small_direct && !c->collective()) {
+        // the batch in k_small's kernel arguments: no copy to the device at all
+        SmallBatch hb;
+        memcpy(hb.cpu, cpu, sizeof(int32_t) * j);
+        memcpy(hb.mem, mem, sizeof(int32_t) * j);
+        memcpy(hb.gpu, gpu, sizeof(int32_t) * j);
+        memcpy(hb.wall, wall, sizeof(int32_t) * j);
+        memcpy(hb.part, part, sizeof(uint16_t) * j);
+        if (nk) memcpy(hb.nk, nk, sizeof(uint16_t) * j);
+        bool done = false;
+        rc = place_impl(c, j, nullptr, nullptr, nullptr, nullptr, nullptr, nk, kmax, c->out.p, stats, out, &done,
+                        &hb);
+        if (rc) return rc;
+        if (!done) return fail(FIT_E_HIP, "direct placement did not return its placements");
+        return 0;
+    }
     const int32_t *dcpu, *dmem, *dgpu, *dwall;
     const uint16_t *dpart, *dk = nullptr;
     const size_t b = sizeof(int32_t) * j, bh = sizeof(uint16_t) * j;

@@ -146,6 +146,14 @@ struct SmallComps {
     int32_t nb[33];
 };
 
+// A small batch carried in k_small's kernel arguments (fit_place: no copy to the device; the
+// kernarg segment holds up to 4 KB, this is 2,560 B).
+constexpr int SMALL_ARGJ = 128;
+struct SmallBatch {
+    int32_t cpu[SMALL_ARGJ], mem[SMALL_ARGJ], gpu[SMALL_ARGJ], wall[SMALL_ARGJ];
+    uint16_t part[SMALL_ARGJ], nk[SMALL_ARGJ];
+};
+
 // Persistent engines' watchdog trip record (fit_engine_ctl.h; read back by engine.cpp).
 enum TripSite : unsigned {
     TRIP_NONE = 0,

@@ -420,8 +420,8 @@ __device__ __forceinline__ int small_place_job_regs(NodeRec* rec, int nb, int rp
     return 1;
 }
 
-__global__ __launch_bounds__(SMALL_THREADS) void k_small(
-    NodeRec* rec, SmallComps C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np,
+__device__ __forceinline__ void small_body(
+    NodeRec* rec, const SmallComps& C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np,
     const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
     const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
     const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t nj, int32_t kmax,
@@ -537,6 +537,42 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_small(
             stat[1] = 0;
         }
     }
+}
+
+__global__ __launch_bounds__(SMALL_THREADS) void k_small(
+    NodeRec* rec, SmallComps C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np,
+    const int32_t* __restrict__ jcpu, const int32_t* __restrict__ jmem,
+    const int32_t* __restrict__ jgpu, const int32_t* __restrict__ jwall,
+    const uint16_t* __restrict__ jpart, const uint16_t* __restrict__ jk, int32_t nj, int32_t kmax,
+    int32_t* __restrict__ out, int32_t* __restrict__ stat) {
+    small_body(rec, C, ncomp, ptab, np, jcpu, jmem, jgpu, jwall, jpart, jk, nj, kmax, out, stat);
+}
+
+// The batch in the kernel arguments (nj <= SMALL_ARGJ): copied into LDS first, then as k_small.
+__global__ __launch_bounds__(SMALL_THREADS) void k_small_args(
+    NodeRec* rec, SmallComps C, int32_t ncomp, const int32_t* __restrict__ ptab, int32_t np, SmallBatch B,
+    int32_t has_nk, int32_t nj, int32_t kmax, int32_t* __restrict__ out, int32_t* __restrict__ stat) {
+    __shared__ SmallBatch sb;
+    for (int i = threadIdx.x; i < nj; i += SMALL_THREADS) {
+        sb.cpu[i] = B.cpu[i];
+        sb.mem[i] = B.mem[i];
+        sb.gpu[i] = B.gpu[i];
+        sb.wall[i] = B.wall[i];
+        sb.part[i] = B.part[i];
+        sb.nk[i] = B.nk[i];
+    }
+    __syncthreads();
+    small_body(rec, C, ncomp, ptab, np, sb.cpu, sb.mem, sb.gpu, sb.wall, sb.part, has_nk ? sb.nk : nullptr, nj, kmax,
+               out, stat);
+}
+
+hipError_t launch_small_args(hipStream_t st, int ncomp, NodeRec* rec, const SmallComps& C, const int32_t* ptab,
+                             int32_t np, const SmallBatch& B, bool has_nk, int32_t nj, int32_t kmax, int32_t* out,
+                             int32_t* stat) {
+    if (nj > SMALL_ARGJ) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_small_args, dim3(ncomp > 0 ? ncomp : 1), dim3(SMALL_THREADS), 0, st, rec, C, ncomp, ptab,
+                       np, B, has_nk ? 1 : 0, nj, kmax, out, stat);
+    return hipGetLastError();
 }
 
 // grid: max(ncomp, 1) blocks (block 0 initialises the rows of jobs that no component owns)
