@@ -102,7 +102,9 @@ typedef struct {
     int32_t shard_mode;    /* mode used (FIT_SHARD_NODES / FIT_SHARD_COMPONENTS; 0 if world 1) */
     int32_t components;    /* independent partition components                               */
     int32_t engine;        /* 1: persistent single-launch engine (k_engine); 0: host-driven rounds; */
-                           /* 2: direct small placement (k_small, <= FIT_SMALL_DIRECT jobs)          */
+                           /* 2: direct small placement (k_small, <= FIT_SMALL_DIRECT jobs);         */
+                           /* 3: demand-class engine (k_class: by default when the live jobs are at  */
+                           /*    least half multi-node; FIT_CLASS=1 / 0 forces it on / off)          */
     int32_t reserved;
     double ms_arb_wait;    /* host time waiting for the device's persistent-launch lock: one   */
                            /* persistent launch per GPU at a time, across contexts and processes */

@@ -342,11 +342,13 @@ struct fit_ctx {
     // the device), and the call spins on the batch's completion event instead of sleeping in a
     // stream synchronisation (FIT_SMALL_ARGS=0 / FIT_SYNC_SPIN=0: A/B switches)
     bool small_args = true, sync_spin = true;
-    // the demand-class engine (fit_class.hip): 0 off (the default, and FIT_ENGINE=persistent|rounds|
+    // the demand-class engine (fit_class.hip): 0 off (FIT_CLASS=0, and FIT_ENGINE=persistent|rounds|
     // direct), 1 for placements the persistent engine would run (FIT_CLASS=1), 2 at every size
-    // (FIT_ENGINE=class);
-    // used when every component is one partition, fits LDS and has <= class_max() demand classes
-    int cls_mode = 0;
+    // (FIT_ENGINE=class), 3 (the default) for those of them whose live jobs are at least half
+    // multi-node; used when every component is one partition, fits LDS and has <= class_max()
+    // demand classes
+    int cls_mode = 3;
+    int32_t last_multi = 0;          // multi-node jobs of the last job lists (build_job_lists)
     bool cls_nodes_ok = false;       // node table: single-partition components that fit LDS
     int32_t cls_maxn = 0;            // largest component (nodes)
     DBuf<int16_t> jcls;
@@ -849,13 +851,14 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
     hipStream_t st = c->st;
     if (c->jl.ensure(std::max(J, 1)) || c->jpk.ensure(J + 1) ||
         c->jls.ensure(std::max<size_t>(joblists_scratch_ints(J), 1) + 2 * (C + 1) + 2) ||
-        c->h_jls.ensure(C + 1 + 2))
+        c->h_jls.ensure(2 * (C + 1) + 2))
         return FIT_E_OOM;
     int32_t* g = c->jls.p + joblists_scratch_ints(J);
     int32_t* jbd = g + 2;
     int32_t* mbd = jbd + C + 1;
     HIP_TRY(launch_joblists(st, c->jcomp.p, J, C, c->jls.p, g, jbd, mbd, c->jl.p, c->jpk.p));
-    HIP_TRY(hipMemcpyAsync(c->h_jls.p, g, sizeof(int32_t) * (C + 3), hipMemcpyDeviceToHost, st));
+    // the counters, the component offsets and the multi-node offsets (mbd[C]: multi-node jobs)
+    HIP_TRY(hipMemcpyAsync(c->h_jls.p, g, sizeof(int32_t) * (2 * (C + 1) + 2), hipMemcpyDeviceToHost, st));
     if (classify) {
         const size_t ts = (size_t)C * class_table_slots() * class_slot_bytes();
         if (c->jcls.ensure(std::max(J, 1)) || c->cls_tab.ensure(ts) ||
@@ -876,7 +879,30 @@ int build_job_lists(fit_ctx* c, int32_t J, fit_stats& S, std::vector<int32_t>& j
     }
     S.rejected = c->h_jls.p[0];
     jb.assign(c->h_jls.p + 2, c->h_jls.p + 2 + C + 1);
+    c->last_multi = c->h_jls.p[2 + C + 1 + C];
     for (int k = 0; k < C; ++k) S.useful_evals += (int64_t)(jb[k + 1] - jb[k]) * c->n;
+    return 0;
+}
+
+// The demand classes of every component's jobs on their own (after build_job_lists, which counted
+// the multi-node jobs the automatic choice needs): k_classify and one synchronisation.
+int classify_jobs(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, const int32_t* gpu,
+                  const uint16_t* part, bool* cls_ok) {
+    const int C = c->ncomp;
+    hipStream_t st = c->st;
+    const size_t ts = (size_t)C * class_table_slots() * class_slot_bytes();
+    if (c->jcls.ensure(std::max(J, 1)) || c->cls_tab.ensure(ts) || c->cls_dem.ensure((size_t)C * class_max()) ||
+        c->cls_n.ensure(C) || c->h_cls_n.ensure(C))
+        return FIT_E_OOM;
+    HIP_TRY(hipMemsetAsync(c->cls_tab.p, 0, ts, st));
+    HIP_TRY(hipMemsetAsync(c->cls_n.p, 0, sizeof(int32_t) * C, st));
+    HIP_TRY(launch_classify(st, c->jcomp.p, cpu, mem, gpu, part, J, c->cls_tab.p, c->cls_dem.p, c->cls_n.p,
+                            c->jcls.p));
+    HIP_TRY(hipMemcpyAsync(c->h_cls_n.p, c->cls_n.p, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *cls_ok = true;
+    for (int k = 0; k < C; ++k)
+        if (c->h_cls_n.p[k] > class_max()) *cls_ok = false;
     return 0;
 }
 
@@ -966,12 +992,20 @@ int place_impl(fit_ctx* c, int32_t J, const int32_t* cpu, const int32_t* mem, co
     const int pre_mode = !c->collective() ? 0
                          : (c->shard_mode == FIT_SHARD_AUTO ? (C >= c->world ? FIT_SHARD_COMPONENTS : FIT_SHARD_NODES)
                                                             : c->shard_mode);
-    const bool try_cls = c->cls_mode > 0 && c->cls_nodes_ok && pre_mode != FIT_SHARD_NODES &&
-                         (c->cls_mode == 2 || J > c->small_batch);
+    const bool cls_able = c->cls_nodes_ok && pre_mode != FIT_SHARD_NODES;
+    const bool try_cls = (c->cls_mode == 1 || c->cls_mode == 2) && cls_able && (c->cls_mode == 2 || J > c->small_batch);
     bool cls_ok = false;
     int rc0 = build_job_lists(c, J, S, jb, cpu, mem, gpu, part, try_cls, &cls_ok);
     if (rc0) return rc0;
-    const bool use_cls = cls_ok && (c->cls_mode == 2 || J - S.rejected > c->small_batch);
+    // automatic (cls_mode 3, the default): a large placement whose live jobs are mostly multi-node
+    // (C4) runs the class engine — its all-picks-at-once commit beats the persistent engine's
+    // single-wave commit there; k = 1 queues keep the persistent engine
+    const int32_t live = J - S.rejected;
+    if (c->cls_mode == 3 && cls_able && live > c->small_batch && 2 * (int64_t)c->last_multi >= live) {
+        rc0 = classify_jobs(c, J, cpu, mem, gpu, part, &cls_ok);
+        if (rc0) return rc0;
+    }
+    const bool use_cls = cls_ok && (c->cls_mode == 2 || live > c->small_batch);
 
     // world > 1: split by components (each rank owns whole components, no per-round exchange)
     // or by nodes (north_star: every rank scans 1/world of every component, RCCL each round)
@@ -1542,7 +1576,7 @@ int fit_create(const fit_opts* opts, fit_ctx** out_ctx) {
     if (const char* ev = getenv("FIT_SMALL_ARGS")) c->small_args = atoi(ev) != 0;
     if (const char* ev = getenv("FIT_SYNC_SPIN")) c->sync_spin = atoi(ev) != 0;
     // FIT_ENGINE forces one engine at every size: "rounds", "persistent" or "direct" (k_small)
-    if (const char* ev = getenv("FIT_CLASS")) c->cls_mode = atoi(ev) ? 1 : 0;
+    if (const char* ev = getenv("FIT_CLASS")) c->cls_mode = atoi(ev) ? 1 : 0;  // unset: automatic (3)
     if (const char* ev = getenv("FIT_ENGINE")) {
         c->persistent = strcmp(ev, "rounds") != 0;
         if (strcmp(ev, "persistent") == 0 || strcmp(ev, "class") == 0) c->small_batch = -1;

@@ -1,4 +1,5 @@
-// fit_class.hip — the demand-class engine.
+// fit_class.hip — the demand-class engine: the default for
+// placements whose live jobs are mostly multi-node (engine.cpp cls_mode 3), opt-in otherwise.
 //
 // A component's pending queue has few distinct per-node demands: a job's CLASS is its (cpu, mem,
 // gpu) of one partition (the reference derives them from a handful of labels,
@@ -50,6 +51,7 @@ constexpr int CLS_TS = 512;                  // classify hash slots per componen
 constexpr int CLS_POOL = CLS_THREADS;        // refill pool (one key per thread at most)
 constexpr int CLS_BK = 3;                    // bookkeeper waves
 constexpr int CLS_JR = 256;                  // staged job ring (wave 4 → the decider)
+constexpr int CLS_PROBE = 4;                 // a full set's insert: slots probed for a dead entry
 constexpr unsigned CLS_SPIN = 1u << 26;      // spin bound of an in-block wait (a bug, not a load)
 
 enum : unsigned { CLS_OP_EXIT = 1, CLS_OP_REFILL = 2, CLS_OP_PICK = 3 };
@@ -246,7 +248,8 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
 #pragma unroll
         for (int i = 1; i < 8; ++i) B = umin64(B, S->ctl.red[0][i]);
         // every node of this thread other than k1 is >= its k2 >= B: the threads' k1 below B are
-        // every node below B
+        // every node below B (≈ 32 of them: a set with room, so the bookkeepers' inserts do not
+        // lower the bound at once — three keys per thread filled the set and doubled the refills)
         if (k1 < B) {
             const unsigned idx = atomicAdd(&S->ctl.pool_n, 1u);
             S->pool[idx] = k1;
@@ -415,9 +418,10 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
 
     if (wave == 0) {
         // ================= DECIDER =================
-        // Software-pipelined: while job t is decided, the next job's class header, demand, set
-        // entries and bookkeeper progress (A) and its candidates' rows (B) are already in flight;
-        // job t's commits then patch the rows B read (a picked node's new row) and the ring lanes.
+        // While job t is decided, the next job's class header, demand, set entries and bookkeeper
+        // progress (A) are already in flight; its candidates' rows (B) are read after job t's
+        // commits, so they are current.  A k-node job commits all its picks at once, one lane
+        // each (its row from LDS, its record, its new row) with one count store.
         ClsDec D{0u, 0u, false};
         int64_t placed = 0, refills = 0, picks = 0, lowers = 0, evals = 0;
 #ifdef FIT_STAMPS
@@ -474,17 +478,15 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
             const int32_t p = lane < CLS_SET ? (lane < cnt ? a.sp : -1) : rpos;
             return p < n ? p : -1;
         };
-        // the job's picks, parked one per lane (lane j = pick j): key and the lane that held it
+        // the job's picks, parked one per lane (lane j = pick j's position; pick 0 in x0)
         uint32_t pkl = 0;
-        int32_t pkn = -1;
         // query: the k smallest distinct candidate keys; returns how many were found and the k-th
-        int32_t x0 = 0, ln0 = 0;  // the first pick (SGPRs): a k = 1 job parks nothing
+        int32_t x0 = 0;  // the first pick (SGPR): a k = 1 job parks nothing
         auto extract = [&](uint64_t key, int k, uint64_t& kth) {
             int ln = 0;
             uint64_t m = wave_min_key_lane(key, ln);
             kth = m;
             x0 = (int32_t)(uint32_t)m;
-            ln0 = ln;
             if (m == KEY_INF) return 0;
             int np = 1;
             for (int j = 1; j < k; ++j) {  // uniform; multi-node jobs only
@@ -492,7 +494,6 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                 m = wave_min_key_lane(key, ln);
                 if (m == KEY_INF) break;
                 pkl = (uint32_t)cls_writelane((int)(uint32_t)m, j, (int)pkl);
-                pkn = cls_writelane(ln, j, pkn);
                 kth = m;
                 np = j + 1;
             }
@@ -503,8 +504,6 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
         QA A{0u, 0ull, make_int4(0, 0, 0, 0), -1, make_uint4(0, 0, 0, 0)};
         int32_t pos = -1;
         int4 row = make_int4(0, 0, 0, 0);
-        bool pf = false;  // this lane's candidate row was patched by a commit after its read
-        int4 prow = make_int4(0, 0, 0, 0);
         if (t0j < t1j) {
             F = conv(ring_at(t0j));
             if (t0j + 1 < t1j) F1 = conv(ring_at(t0j + 1));
@@ -520,14 +519,12 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                 break;
             }
             const bool has_next = t + 1 < t1j;
-            // ---- query job t: its candidates' keys first (the rows arrived during the previous
-            // step; waiting for them now waits for nothing issued since)
+            // ---- query job t: its candidates' keys first (the rows were read at the end of the
+            // previous step, after its commits: current, nothing to patch)
             const int4 d = make_int4(__builtin_amdgcn_readfirstlane(A.d.x), __builtin_amdgcn_readfirstlane(A.d.y),
                                      __builtin_amdgcn_readfirstlane(A.d.z), 0);
             uint64_t Lc = rdlane64(A.L, 0);
-            const int4 r0 = make_int4(pf ? prow.x : row.x, pf ? prow.y : row.y, pf ? prow.z : row.z,
-                                      pf ? prow.w : row.w);
-            const uint64_t key0 = pos >= 0 ? cls_key<true>(r0, d.x, d.y, d.z, F.w, (uint32_t)pos) : KEY_INF;
+            const uint64_t key0 = pos >= 0 ? cls_key<true>(row, d.x, d.y, d.z, F.w, (uint32_t)pos) : KEY_INF;
             asm volatile("" ::"v"((uint32_t)key0), "v"((uint32_t)(key0 >> 32)) : "memory");
             CLS_T(tq1);
             // then A(t+1) and job t+3's fields, in flight during the extraction
@@ -543,7 +540,6 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
             // the k-th pick below the bound, or the bound infinite: exact (np < k: unplaced)
             bool certified = Lc == KEY_INF || (np == F.k && kth < Lc);
             CLS_T(tj1);
-            int4 rq = r0;  // the rows the picks' lanes hold
             if (!certified) {
                 // ---- exhausted: the workgroup refills the class's set and the job is queried
                 // again; if the walltime or k still defeats the fresh set it is resolved exactly
@@ -557,7 +553,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                 evals += n;
                 A = load_a(F.cl);
                 pos = cand_pos(A);
-                rq = rows[pos >= 0 ? pos : 0];
+                const int4 rq = rows[pos >= 0 ? pos : 0];
                 Lc = rdlane64(A.L, 0);
                 np = extract(pos >= 0 ? cls_key<true>(rq, d.x, d.y, d.z, F.w, (uint32_t)pos) : KEY_INF, F.k, kth);
                 evals += 64;
@@ -566,30 +562,20 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                     cls_request(S, D, CLS_OP_PICK, (unsigned)F.cl, F.w, (unsigned)F.k);
                     cls_block_op(S, rows, n, tid);
                     np = (int)S->ctl.npick;
-                    // lane j < np: pick j, its row in rq (the commit reads picks' rows by lane)
+                    // lane j < np: pick j
                     const uint64_t m = lane < np ? S->ctl.pick[lane < FIT_KMAX ? lane : 0] : 0ull;
                     pkl = (uint32_t)m;
-                    pkn = lane;
                     x0 = (int32_t)(uint32_t)S->ctl.pick[0];
-                    ln0 = 0;
-                    rq = rows[lane < np ? (int32_t)(uint32_t)m : 0];
                     ++picks;
                     evals += (int64_t)F.k * n;
                 }
                 reload_next = true;  // a refill may have replaced the next job's set
             }
             CLS_T(tj2);
-            // ---- B(t+1): the next job's candidate rows, read before this job's commits (patched)
-            int32_t pos1 = -1;
-            int4 row1 = make_int4(0, 0, 0, 0);
-            bool pf1 = false;
-            int4 prow1 = make_int4(0, 0, 0, 0);
-            if (has_next && !reload_next) {
-                pos1 = cand_pos(A1);
-                row1 = rows[pos1 >= 0 ? pos1 : 0];
-            }
             CLS_T(tb1);
-            // ---- commit job t (all or nothing: np == k)
+            // ---- commit job t (all or nothing: np == k), every pick at once: lane j < k takes
+            // pick j — its current row from LDS (each pick is a distinct node), its record in
+            // ring slot ncommit + j, its new row; then one count store for all of them
             if (np == F.k) {
                 ++placed;
                 {  // every record slot this job writes must be free (all bookkeepers past it)
@@ -608,51 +594,36 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                         break;
                     }
                 }
-                for (int j = 0; j < F.k; ++j) {  // uniform
-                    const int32_t x = j == 0 ? x0 : __builtin_amdgcn_readlane((int)pkl, j);
-                    const int ln = j == 0 ? ln0 : __builtin_amdgcn_readlane(pkn, j);
-                    // the row the query used (current: each pick is a distinct node)
-                    int4 o;
-                    o.x = __builtin_amdgcn_readlane(rq.x, ln);
-                    o.y = __builtin_amdgcn_readlane(rq.y, ln);
-                    o.z = __builtin_amdgcn_readlane(rq.z, ln);
-                    o.w = __builtin_amdgcn_readlane(rq.w, ln);
-                    const int4 nw = make_int4(o.x - d.x, o.y - d.y, o.z - d.z, o.w);
-                    // lane 0 stores the record, the count and the row; lanes 1..63 store into their
-                    // own sink slots (no branch on the chain, no bank conflict)
-                    ClsRec* rp = lane == 0 ? &S->rec[D.ncommit & (CLS_REC - 1)] : &S->sink[lane];
-                    *reinterpret_cast<int4*>(&rp->x) = make_int4(x, o.x, o.y, o.z);
-                    *reinterpret_cast<int4*>(&rp->nc) = make_int4(nw.x, nw.y, nw.z, F.q * kmax + j);
-                    CLS_CBAR();  // record, then the count (one wave's LDS operations run in order)
-                    ++D.ncommit;
-                    *(lane == 0 ? &S->ctl.ncommit : reinterpret_cast<unsigned*>(&S->sink[lane].oc)) = D.ncommit;
-                    *(lane == 0 ? &rows[x] : reinterpret_cast<int4*>(&S->sink[lane].nc)) = nw;
-                    const int slot = CLS_SET + (int)((D.ncommit - 1) & (CLS_RING - 1));
-                    if (lane == slot) rpos = x;
-                    // the next job's candidates: this node's new row, and the ring lane it took
-                    const bool hit = pos1 == x || lane == slot;
-                    if (lane == slot) pos1 = has_next && !reload_next ? x : -1;
-                    pf1 = pf1 || hit;
-                    prow1.x = hit ? nw.x : prow1.x;  // per field: a select of the int4 became a
-                    prow1.y = hit ? nw.y : prow1.y;  // scratch round trip (and a vmcnt(0) wait)
-                    prow1.z = hit ? nw.z : prow1.z;
-                    prow1.w = hit ? nw.w : prow1.w;
-                    // (a later pick of this job replaces an earlier one's row only on its own node)
-                    evals += 2 * (int64_t)ncls;  // the bookkeepers' old / new key of every class
+                const bool pk = lane < F.k;
+                const int32_t xl = lane == 0 ? x0 : (int32_t)pkl;  // lane j < k: pick j's position
+                const int4 o = rows[pk ? xl : 0];
+                const int4 nw = make_int4(o.x - d.x, o.y - d.y, o.z - d.z, o.w);
+                // lanes past k store into their own sink slots (no branch on the chain)
+                ClsRec* rp = pk ? &S->rec[(D.ncommit + (unsigned)lane) & (CLS_REC - 1)] : &S->sink[lane];
+                *reinterpret_cast<int4*>(&rp->x) = make_int4(xl, o.x, o.y, o.z);
+                *reinterpret_cast<int4*>(&rp->nc) = make_int4(nw.x, nw.y, nw.z, F.q * kmax + lane);
+                CLS_CBAR();  // records, then the count (one wave's LDS operations run in order)
+                const unsigned n0 = D.ncommit;
+                D.ncommit += (unsigned)F.k;
+                *(lane == 0 ? &S->ctl.ncommit : reinterpret_cast<unsigned*>(&S->sink[lane].oc)) = D.ncommit;
+                *(pk ? &rows[xl] : reinterpret_cast<int4*>(&S->sink[lane].nc)) = nw;
+                // ring lanes CLS_SET..63: commit n0 + j lands in lane CLS_SET + ((n0 + j) & 7)
+                const int jr = (int)(((unsigned)(lane - CLS_SET) - n0) & (unsigned)(CLS_RING - 1));
+                const int32_t xr = __builtin_amdgcn_ds_bpermute(jr << 2, xl);
+                if (lane >= CLS_SET && jr < F.k) rpos = xr;
+                evals += 2 * (int64_t)ncls * F.k;  // the bookkeepers' old / new key of every class
 #ifdef FIT_STAMPS
-                    st_acc[7] += 1;
+                st_acc[7] += (unsigned long long)F.k;
 #endif
-                }
-                if (D.fail) break;
             }
             CLS_T(tj3);
 #ifdef FIT_STAMPS
-            st_acc[1] += tq1 - tj0;   // head: patch, key
+            st_acc[1] += tq1 - tj0;   // head: key
             st_acc[3] += tq2 - tq1;   // A(t+1) issue, ring
             st_acc[0] += tj1 - tq2;   // extraction, certification
             st_acc[2] += tj2 - tj1;
-            st_acc[5] += tb1 - tj2;   // B(t+1): positions (waits for A), rows issue
-            st_acc[4] += tj3 - tb1;
+            st_acc[5] += tb1 - tj2;
+            st_acc[4] += tj3 - tb1;   // commit
             st_acc[6] += 1;
 #endif
             if (!has_next) break;
@@ -675,20 +646,14 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                     CLS_T(tw1);
                 }
             }
-            if (reload_next) {  // re-read A and B for the next job now (current rows, ring)
-                A1 = load_a(F1.cl);
-                pos1 = cand_pos(A1);
-                row1 = rows[pos1 >= 0 ? pos1 : 0];
-                pf1 = false;
-            }
+            if (reload_next) A1 = load_a(F1.cl);  // re-read A for the next job now
+            // B(t+1): the next job's candidate rows, after this job's commits (current rows)
+            pos = cand_pos(A1);
+            row = rows[pos >= 0 ? pos : 0];
             F = F1;
             F1 = conv(rj2);
             rj2 = rj3;
             A = A1;
-            pos = pos1;
-            row = row1;
-            pf = pf1;
-            prow = prow1;
         }
         // drain, then the exit op (a failed drain still exits: the error word says why)
         const bool drained = cls_drain(S, D.ncommit);
@@ -721,6 +686,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
         const int4 d = valid ? S->dem[cls] : make_int4(0, 0, 0, 0);
         uint64_t myL = valid ? S->hdr[cls].L : 0ull;
         unsigned mycnt = valid ? S->hdr[cls].cnt : 0u;
+        unsigned probe_at = 0;  // the next set slot a full set's insert probes for a dead entry
         unsigned p = 0, ep = 0;
         for (;;) {
             const unsigned nc = lds_ld(&S->ctl.ncommit);
@@ -743,8 +709,26 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                             CLS_CBAR();  // entry, then count
                             lds_st(&S->hdr[cls].cnt, mycnt);
                         } else {
-                            myL = kn;  // full: the bound falls to x's key, x stays out
-                            S->hdr[cls].L = kn;
+                            // full: x takes the slot of a dead entry — a node the class no longer
+                            // fits at the current rows, which only shrink (a torn row read mixes
+                            // old and new values, so "does not fit" is never wrong) — found among
+                            // a few probes from a rotating cursor; else the bound falls to x's key
+                            // and x stays out.  A concurrent query sees the dead node or x (x is in
+                            // the decider's ring): either is harmless.
+                            bool took = false;
+                            for (int pr = 0; pr < CLS_PROBE && !took; ++pr) {
+                                const unsigned i = probe_at;
+                                probe_at = probe_at + 1u < (unsigned)CLS_SET ? probe_at + 1u : 0u;
+                                const int y = S->set[cls][i];
+                                if (cls_key<false>(rows[y], d.x, d.y, d.z, 0, (uint32_t)y) == KEY_INF) {
+                                    S->set[cls][i] = (uint16_t)R.x;
+                                    took = true;
+                                }
+                            }
+                            if (!took) {
+                                myL = kn;
+                                S->hdr[cls].L = kn;
+                            }
                         }
                     }
                 }

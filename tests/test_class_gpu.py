@@ -149,7 +149,8 @@ def test_class_fuzz(seed, monkeypatch):
 def test_class_is_the_production_choice(monkeypatch):
     """FIT_CLASS=1, FIT_ENGINE unset: a large placement on single-partition components runs the
     class engine; overlapping partitions (c3o: one component) keep the persistent engine; without
-    FIT_CLASS (the default) the persistent engine runs; a small one stays on the rounds."""
+    FIT_CLASS (automatic) a k = 1 queue runs the persistent engine; a small one stays on the
+    rounds."""
     monkeypatch.delenv("FIT_ENGINE", raising=False)
     monkeypatch.setenv("FIT_CLASS", "1")
     nodes, jobs, parts = synth.make_config("c3", 20000, 40000)
@@ -161,6 +162,19 @@ def test_class_is_the_production_choice(monkeypatch):
     monkeypatch.delenv("FIT_CLASS", raising=False)
     nodes, jobs, parts = synth.make_config("c3", 20000, 40000)
     _check(nodes, jobs, parts, engine_id=1)
+
+
+@pytest.mark.auto_engine
+def test_class_is_the_default_for_multi_node_queues(monkeypatch):
+    """FIT_CLASS and FIT_ENGINE unset: a large placement whose live jobs are mostly multi-node (C4:
+    75 %) runs the class engine (its all-picks-at-once commit beats the single-wave commit there);
+    FIT_CLASS=0 keeps the persistent engine; a k = 1 queue keeps it too (previous test)."""
+    monkeypatch.delenv("FIT_ENGINE", raising=False)
+    monkeypatch.delenv("FIT_CLASS", raising=False)
+    nodes, jobs, parts = synth.make_config("c4", 8192, 30000)
+    _check(nodes, jobs, parts, kmax=8, engine_id=3)
+    monkeypatch.setenv("FIT_CLASS", "0")
+    _check(nodes, jobs, parts, kmax=8, engine_id=1)
 
 
 def test_class_consecutive_placements(monkeypatch):

@@ -27,7 +27,7 @@ with Engine() as e:
     buf = (C.c_ulonglong * (32 * 8))()
     assert _lib.lib().fit_debug_class_stamps(buf) == 0
 print(name, {k: st[k] for k in ("engine", "placed", "unplaced", "rounds", "stops_rescan", "ms_device", "ms_commit")})
-names = ["extract+certify", "head: patch+key", "refill / pick", "A issue + ring", "commit", "B: wait A, issue rows"]
+names = ["extract+certify", "head: key (rows of B)", "refill / pick", "A issue + ring", "commit", "-"]
 rows = [list(buf[c * 8:(c + 1) * 8]) for c in range(32)]
 rows = [r for r in rows if r[6]]
 longest = max(rows, key=lambda r: sum(r[:6]))
