@@ -51,7 +51,10 @@ constexpr int CLS_TS = 512;                  // classify hash slots per componen
 constexpr int CLS_POOL = CLS_THREADS;        // refill pool (one key per thread at most)
 constexpr int CLS_BK = 3;                    // bookkeeper waves
 constexpr int CLS_JR = 256;                  // staged job ring (wave 4 → the decider)
-constexpr int CLS_PROBE = 4;                 // a full set's insert: slots probed for a dead entry
+#ifndef CLS_PROBES
+#define CLS_PROBES 16
+#endif
+constexpr int CLS_PROBE = CLS_PROBES;        // a full set's insert: slots probed for a dead entry
 constexpr unsigned CLS_SPIN = 1u << 26;      // spin bound of an in-block wait (a bug, not a load)
 
 enum : unsigned { CLS_OP_EXIT = 1, CLS_OP_REFILL = 2, CLS_OP_PICK = 3 };

@@ -1,18 +1,19 @@
 #!/bin/bash
-# Round 6: the class engine's decider with all of a job's picks committed at once — its GPU tests,
-# a paired A/B against the previous decider (fitgpu/libfitgpu_clsold.so) with FIT_ENGINE=class on
-# C4 / C3 / C2, the persistent engine beside it, and the stamps build's per-segment cycles.
+# Round 6: class engine (k_class) A/Bs — its GPU tests, a paired A/B of the current build against a
+# variant library ($2, default fitgpu/libfitgpu_clsold.so) with FIT_ENGINE=class on C4 / C3 / C2,
+# the default engine choice beside it, and the stamps build's per-segment cycles.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${1:-r06w}
+VAR=${2:-slurm-bridge-operator_amd/fitgpu/libfitgpu_clsold.so}
 timeout -k 10 600 python -u -m pytest tests/test_class_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.txt 2>&1 || { tail -30 gpurun_out/${T}_tests.txt; exit 1; }
 tail -1 gpurun_out/${T}_tests.txt
 Q="--no-cpu --no-live-pmc --no-shard-price --no-device-path --steps 5 --warmup 2 --repeats 1"
 for i in 1 2; do
   for w in c4 c3 c2; do
     FIT_ENGINE=class timeout -k 10 300 python -u bench.py --workload $w $Q > gpurun_out/${T}_${w}_new_$i.json 2> gpurun_out/${T}_${w}_new_$i.err || { tail -5 gpurun_out/${T}_${w}_new_$i.err; exit 1; }
-    FIT_ENGINE=class FITGPU_LIB=slurm-bridge-operator_amd/fitgpu/libfitgpu_clsold.so timeout -k 10 300 python -u bench.py --workload $w $Q > gpurun_out/${T}_${w}_old_$i.json 2> gpurun_out/${T}_${w}_old_$i.err || { tail -5 gpurun_out/${T}_${w}_old_$i.err; exit 1; }
+    FIT_ENGINE=class FITGPU_LIB=$VAR timeout -k 10 300 python -u bench.py --workload $w $Q > gpurun_out/${T}_${w}_old_$i.json 2> gpurun_out/${T}_${w}_old_$i.err || { tail -5 gpurun_out/${T}_${w}_old_$i.err; exit 1; }
   done
 done
 for w in c4 c3; do
