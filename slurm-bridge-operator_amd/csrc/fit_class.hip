@@ -69,11 +69,18 @@ enum : unsigned { CLS_OP_EXIT = 1, CLS_OP_REFILL = 2, CLS_OP_PICK = 3 };
 // fit_debug_class_stamps: [0] bookkeeper wait, [1] query, [2] refill (drain + op), [3] exact pick,
 // [4] commit, [5] job-chunk loads, [6] jobs, [7] commits
 __device__ unsigned long long g_cls_st[32][8];
+// refill phases seen by the decider wave: [0] until barrier A, [1] scan + B1, [2] pool + B2,
+// [3] set build (wave 0), [4] barrier C, [5] refills
+__device__ unsigned long long g_cls_op[32][8];
+#define CLS_OPT(v) const unsigned long long v = (wave == 0) ? __builtin_amdgcn_s_memtime() : 0ull
+#define CLS_OPADD(i, a, b) do { if (tid == 0) atomicAdd(&g_cls_op[blockIdx.x & 31][i], (b) - (a)); } while (0)
 #define CLS_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define CLS_ACC(i, a, b) (st_acc[i] += (b) - (a))
 #else
 #define CLS_T(v)
 #define CLS_ACC(i, a, b)
+#define CLS_OPT(v)
+#define CLS_OPADD(i, a, b)
 #endif
 
 struct ClsSlot {  // classify hash slot (global, 32 B)
@@ -227,7 +234,9 @@ __global__ __launch_bounds__(256) void k_classify(const int8_t* __restrict__ jco
 // is built).  PICK: the k smallest keys with the walltime, in ctl.pick[0..npick).
 __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, int32_t n, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
+    CLS_OPT(o0);
     __syncthreads();  // A: the op's parameters
+    CLS_OPT(o1);
     const unsigned op = S->ctl.op;
     if (op == CLS_OP_EXIT) return op;
     const unsigned cl = S->ctl.op_cls;
@@ -247,6 +256,7 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
         const uint64_t m = wave_min_key(k2);
         if (lane == 0) S->ctl.red[0][wave] = m;
         __syncthreads();  // B1
+        CLS_OPT(o2);
         uint64_t B = S->ctl.red[0][0];
 #pragma unroll
         for (int i = 1; i < 8; ++i) B = umin64(B, S->ctl.red[0][i]);
@@ -258,6 +268,7 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
             S->pool[idx] = k1;
         }
         __syncthreads();  // B2
+        CLS_OPT(o3);
         if (wave == 0) {
             const unsigned P = S->ctl.pool_n;
             uint64_t e[CLS_POOL / 64];
@@ -310,7 +321,15 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
                 S->hdr[cl].L = T;
             }
         }
+        CLS_OPT(o4);
         __syncthreads();  // C: the new set and bound
+        CLS_OPT(o5);
+        CLS_OPADD(0, o0, o1);
+        CLS_OPADD(1, o1, o2);
+        CLS_OPADD(2, o2, o3);
+        CLS_OPADD(3, o3, o4);
+        CLS_OPADD(4, o4, o5);
+        CLS_OPADD(5, 0ull, 1ull);
         return op;
     }
     // CLS_OP_PICK: exact k smallest with the walltime (extraction r excludes keys <= prev)
@@ -550,6 +569,8 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
                     D.fail = true;
                     break;
                 }
+                CLS_T(tdr);
+                CLS_ACC(5, tj1, tdr);  // stamps: the drain's share of a refill
                 cls_request(S, D, CLS_OP_REFILL, (unsigned)F.cl, 0, 0);
                 cls_block_op(S, rows, n, tid);
                 ++refills;
@@ -625,7 +646,6 @@ __global__ __launch_bounds__(CLS_THREADS) void k_class(
             st_acc[3] += tq2 - tq1;   // A(t+1) issue, ring
             st_acc[0] += tj1 - tq2;   // extraction, certification
             st_acc[2] += tj2 - tj1;
-            st_acc[5] += tb1 - tj2;
             st_acc[4] += tj3 - tb1;   // commit
             st_acc[6] += 1;
 #endif
@@ -824,7 +844,8 @@ __global__ __launch_bounds__(256) void k_class_out(int32_t* __restrict__ out, in
 
 // ---- host-side entry points ---------------------------------------------------------------------
 #ifdef FIT_STAMPS
-extern "C" int fit_debug_class_stamps(unsigned long long* out /* 32 x 8 */) {
+extern "C" int fit_debug_class_stamps(unsigned long long* out /* 2 x 32 x 8: decider, refill phases */) {
+    if (hipMemcpyFromSymbol(out + 32 * 8, HIP_SYMBOL(g_cls_op), sizeof(g_cls_op)) != hipSuccess) return -2;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cls_st), sizeof(g_cls_st)) == hipSuccess ? 0 : -2;
 }
 #endif

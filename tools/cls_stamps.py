@@ -24,17 +24,21 @@ with Engine() as e:
     e.load_nodes(nodes)
     e.load_partitions(parts)
     out, st = e.place(jobs, kmax=kmax)
-    buf = (C.c_ulonglong * (32 * 8))()
+    buf = (C.c_ulonglong * (2 * 32 * 8))()
     assert _lib.lib().fit_debug_class_stamps(buf) == 0
 print(name, {k: st[k] for k in ("engine", "placed", "unplaced", "rounds", "stops_rescan", "ms_device", "ms_commit")})
-names = ["extract+certify", "head: key (rows of B)", "refill / pick", "A issue + ring", "commit", "-"]
+names = ["extract+certify", "head: key (rows of B)", "refill / pick", "A issue + ring", "commit", "  (of refill: drain)"]
 rows = [list(buf[c * 8:(c + 1) * 8]) for c in range(32)]
 rows = [r for r in rows if r[6]]
-longest = max(rows, key=lambda r: sum(r[:6]))
+longest = max(rows, key=lambda r: sum(r[:5]))  # [5] is a part of [2]
 for label, r in (("longest component", longest), ("all components", [sum(x) for x in zip(*rows)])):
     jobs_n, commits = r[6], r[7]
-    tot = sum(r[:6])
+    tot = sum(r[:5])
     print(f"{label}: jobs {jobs_n}, commits {commits}, {tot / max(jobs_n, 1):.0f} cycles/job "
           f"({tot / 2.4e6 / (1 if label.startswith('longest') else len(rows)):.2f} ms at 2.4 GHz)")
     for n, v in zip(names, r[:6]):
         print(f"  {n:16s} {v / max(jobs_n, 1):8.0f} cycles/job  {100 * v / max(tot, 1):5.1f} %")
+op = [sum(buf[32 * 8 + c * 8 + i] for c in range(32)) for i in range(8)]
+nref = max(op[5], 1)
+print(f"refills (all components): {op[5]}, cycles per refill seen by the decider wave: "
+      + ", ".join(f"{n} {v / nref:.0f}" for n, v in zip(["to barrier A", "scan + B1", "pool + B2", "set build", "barrier C"], op[:5])))
