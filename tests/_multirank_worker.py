@@ -19,7 +19,11 @@ def main():
     ap.add_argument("--nodes", type=int, default=20000)
     ap.add_argument("--jobs", type=int, default=100000)
     ap.add_argument("--out")
+    ap.add_argument("--kmax", type=int, default=1)
+    ap.add_argument("--auto-engine", action="store_true", help="the library's own engine choice")
     a = ap.parse_args()
+    if a.auto_engine:
+        os.environ.pop("FIT_ENGINE", None)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(a.port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
@@ -42,10 +46,10 @@ def main():
     with Engine(device=0, rank=a.rank, world=a.world, exchange=x, shard_mode=a.mode) as e:
         e.load_nodes(nodes)
         e.load_partitions(parts)
-        out, st = e.place(jobs)
+        out, st = e.place(jobs, kmax=a.kmax)
         fin = e.read_nodes()
     np.savez(a.out, out=out, cpu=fin[0], mem=fin[1], gpu=fin[2],
-             stats=np.array([st["placed"], st["unplaced"], st["rejected"], st["shard_mode"]]))
+             stats=np.array([st["placed"], st["unplaced"], st["rejected"], st["shard_mode"], st["engine"]]))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -45,6 +45,30 @@ def test_two_ranks_match_oracle(tmp_path, mode, config, nn, jj):
         assert d["stats"][3] == mode
 
 
+def test_two_ranks_multi_node_class_engine(tmp_path):
+    """C4-shaped (75 % multi-node jobs, kmax 8) with the library's own engine choice — the
+    demand-class engine — component-sharded over 2 ranks: each rank places its components, the
+    merge gives both ranks the oracle's placements and node state."""
+    port = free_port()
+    nn, jj = 8192, 30000
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_multirank_worker.py"), "--rank", str(r),
+                               "--world", "2", "--port", str(port), "--mode", str(FIT_SHARD_COMPONENTS),
+                               "--config", "c4", "--nodes", str(nn), "--jobs", str(jj), "--kmax", "8",
+                               "--auto-engine", "--out", str(tmp_path / f"r{r}.npz")])
+             for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    nodes, jobs, parts = synth.make_config("c4", nn, jj)
+    ref, rst, rfin = po.ref_place(nodes, jobs, parts, kmax=8)
+    for r in range(2):
+        d = np.load(tmp_path / f"r{r}.npz")
+        assert d["stats"][4] == 3  # the class engine ran
+        assert np.array_equal(d["out"], ref)
+        for k, col in zip(("cpu", "mem", "gpu"), rfin):
+            assert np.array_equal(d[k], col)
+        assert list(d["stats"][:3]) == [rst["placed"], rst["unplaced"], rst["rejected"]]
+
+
 def test_two_ranks_backfill_match_oracle(tmp_path):
     """C5 (SPEC §2b) node-sharded over 2 ranks: each scans half of every component, candidates and
     bounds are exchanged every round, the commit runs replicated; both ranks equal the oracle."""
