@@ -12,9 +12,10 @@
 //     every node NOT in S_c has key_c >= L_c          (key_c: SPEC §2's key without the walltime
 //                                                      term; the walltime is a per-job filter)
 // Listed keys are evaluated at query time from the current rows, so a commit touches a class only
-// when the committed node x is unlisted and its new key falls below L_c: x joins S_c (room left) or
-// L_c drops to x's key (set full; x stays out, >= the new bound).  Keys only fall within a
-// placement, so an unlisted node whose row did not change stays >= L_c.
+// when the committed node x is unlisted and its new key falls below L_c: x joins S_c (room left),
+// takes the slot of a dead entry (a listed node the class no longer fits: rows only shrink, so it
+// never will again), or L_c drops to x's key (x stays out, >= the new bound).  Keys only fall
+// within a placement, so an unlisted node whose row did not change stays >= L_c.
 //
 // Query of job t (class c, walltime w, k nodes): the candidates are S_c's entries plus the nodes of
 // the last CLS_RING commits (the "ring": commits the class's bookkeeper may not have processed yet),
@@ -25,10 +26,12 @@
 // second key, so again every unlisted node is >= the new L_c) and the job is queried again; if the
 // walltime or k still defeats the set, the workgroup resolves the job by an exact scan.
 //
-// Waves: 0 = DECIDER (the chain: query, commit, record); 1..3 = BOOKKEEPERS (wave 1+b owns classes
+// Waves: 0 = DECIDER (the chain: query, commit — all k picks of a job at once, one lane each —
+// record); 1..3 = BOOKKEEPERS (wave 1+b owns classes
 // [64b, 64b+64), one per lane: for each commit record (x, old row, new row) it decides membership
 // by the old key against its own register copy of L, and appends x or lowers L — the only writer
-// of its classes' sets and bounds); 4..7 join the block operations only (refill, exact pick).
+// of its classes' sets and bounds); 4 = JOB STAGER (the component's job fields into an LDS ring
+// ahead of the decider); 5..7 join the block operations only (refill, exact pick).
 //
 // LDS protocol (workgroup scope, as fit_commit_mw.h): decider → bookkeepers: record, release,
 // ncommit, then the row; bookkeepers: relaxed poll of ncommit, acquire, record.  Bookkeeper →
