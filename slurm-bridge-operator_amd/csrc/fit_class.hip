@@ -167,7 +167,7 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// ---- classify: a dense class id per job and component (one launch over all jobs) ------------
+// ---- classify: a dense class id per job and component (two launches over all jobs) -----------
 __device__ __forceinline__ uint64_t cls_hash(int32_t a, int32_t b, int32_t c, int32_t d) {
     uint64_t z = ((uint64_t)(uint32_t)a << 32 | (uint32_t)b) * 0x9E3779B97F4A7C15ull;
     z ^= ((uint64_t)(uint32_t)c << 32 | (uint32_t)d) + 0xBF58476D1CE4E5B9ull + (z << 6) + (z >> 2);
@@ -176,60 +176,89 @@ __device__ __forceinline__ uint64_t cls_hash(int32_t a, int32_t b, int32_t c, in
     return z ^ (z >> 31);
 }
 
+// Two launches, so that the lookups need no acquire: INSERT puts every distinct (partition, cpu,
+// mem, gpu) of a component into its hash table (the first inserter of a tuple also numbers it and
+// stores its demand); LOOKUP, after the kernel boundary has made the table visible, finds each
+// job's tuple with plain loads and checks it field by field.  Two tuples with one 64-bit tag (the
+// second one's insert stops at the first one's slot) end in a failed lookup, which makes the
+// component ineligible — the placement then runs the persistent engine.
+__device__ __forceinline__ bool cls_job_tuple(int q, const int8_t* __restrict__ jcomp, const int32_t* __restrict__ jcpu,
+                                              const int32_t* __restrict__ jmem, const int32_t* __restrict__ jgpu,
+                                              const uint16_t* __restrict__ jpart, int* c, int4* t) {
+    const int jc = jcomp[q];
+    if (jc < 0) return false;  // rejected or invalid: never placed by the engine
+    *c = jc & 0x3f;            // k_prefilter tags a multi-node job's component with 0x40
+    *t = make_int4(jcpu[q], jmem[q], jgpu[q], jpart[q]);
+    return true;
+}
+
 __global__ __launch_bounds__(256) void k_classify(const int8_t* __restrict__ jcomp,
                                                   const int32_t* __restrict__ jcpu,
                                                   const int32_t* __restrict__ jmem,
                                                   const int32_t* __restrict__ jgpu,
                                                   const uint16_t* __restrict__ jpart, int32_t nj,
                                                   ClsSlot* __restrict__ tab, int4* __restrict__ dem,
-                                                  int32_t* __restrict__ ncls, int16_t* __restrict__ jcls) {
+                                                  int32_t* __restrict__ ncls) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nj) return;
-    const int jc = jcomp[q];
-    if (jc < 0) return;  // rejected or invalid: never placed by the engine
-    const int c = jc & 0x3f;  // k_prefilter tags a multi-node job's component with 0x40
-    const int32_t a = jcpu[q], b = jmem[q], g = jgpu[q], p = jpart[q];
-    const uint64_t h = cls_hash(a, b, g, p);
+    int c;
+    int4 t;
+    if (!cls_job_tuple(q, jcomp, jcpu, jmem, jgpu, jpart, &c, &t)) return;
+    const uint64_t h = cls_hash(t.x, t.y, t.z, t.w);
     const unsigned long long tag = h | 1ull;
     ClsSlot* T = tab + (size_t)c * CLS_TS;
     unsigned s = (unsigned)h & (CLS_TS - 1);
-    int id = -1;
-    // one slot per iteration and no inner spin, so lanes of one wave that wait for a tuple
-    // another lane of the same wave is publishing let that lane run its stores
-    for (unsigned probe = 0; probe < CLS_TS * 64u;) {
+    for (int probe = 0; probe < CLS_TS; ++probe) {
         unsigned long long cur = __hip_atomic_load(&T[s].tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == 0ull) {
             unsigned long long exp = 0ull;
             if (__hip_atomic_compare_exchange_strong(&T[s].tag, &exp, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)) {
-                T[s].cpu = a;
-                T[s].mem = b;
-                T[s].gpu = g;
-                T[s].part = p;
+                T[s].cpu = t.x;
+                T[s].mem = t.y;
+                T[s].gpu = t.z;
+                T[s].part = t.w;
                 const int nid = atomicAdd(&ncls[c], 1);
-                if (nid < CLS_MAX) dem[(size_t)c * CLS_MAX + nid] = make_int4(a, b, g, p);
-                __hip_atomic_store(&T[s].idp, nid + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                id = nid;
-                break;
+                if (nid < CLS_MAX) dem[(size_t)c * CLS_MAX + nid] = t;
+                T[s].idp = nid + 1;  // read by the lookup launch
+                return;
             }
             cur = exp;
         }
-        if (cur == tag) {
-            const int idp = __hip_atomic_load(&T[s].idp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (idp == 0) {  // published soon: look again (bounded by the probe budget)
-                probe += 1;
-                continue;
-            }
-            if (T[s].cpu == a && T[s].mem == b && T[s].gpu == g && T[s].part == p) {
-                id = idp - 1;
-                break;
-            }
+        if (cur == tag) return;  // this tuple (or a tag twin, caught by the lookup) is in
+        s = (s + 1) & (CLS_TS - 1);
+    }
+    atomicMax(&ncls[c], CLS_TS);  // table full: the component is not eligible
+}
+
+__global__ __launch_bounds__(256) void k_classify_lookup(const int8_t* __restrict__ jcomp,
+                                                         const int32_t* __restrict__ jcpu,
+                                                         const int32_t* __restrict__ jmem,
+                                                         const int32_t* __restrict__ jgpu,
+                                                         const uint16_t* __restrict__ jpart, int32_t nj,
+                                                         const ClsSlot* __restrict__ tab,
+                                                         int32_t* __restrict__ ncls, int16_t* __restrict__ jcls) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nj) return;
+    int c;
+    int4 t;
+    if (!cls_job_tuple(q, jcomp, jcpu, jmem, jgpu, jpart, &c, &t)) return;
+    const uint64_t h = cls_hash(t.x, t.y, t.z, t.w);
+    const unsigned long long tag = h | 1ull;
+    const ClsSlot* T = tab + (size_t)c * CLS_TS;
+    unsigned s = (unsigned)h & (CLS_TS - 1);
+    int id = -1;
+    for (int probe = 0; probe < CLS_TS; ++probe) {
+        const ClsSlot& e = T[s];
+        if (e.tag == 0ull) break;
+        if (e.tag == tag) {
+            if (e.cpu == t.x && e.mem == t.y && e.gpu == t.z && e.part == t.w) id = e.idp - 1;
+            break;
         }
         s = (s + 1) & (CLS_TS - 1);
-        probe += 64;  // a full table is given up after CLS_TS distinct slots
     }
     jcls[q] = (int16_t)(id >= 0 && id < CLS_MAX ? id : -1);
-    if (id < 0) atomicMax(&ncls[c], CLS_TS);  // table full: the component is not eligible
+    if (id < 0) atomicMax(&ncls[c], CLS_TS);  // not found (a tag twin): the component is not eligible
 }
 
 // ---- block operations (every wave, between barriers) ------------------------------------------
@@ -865,7 +894,9 @@ hipError_t launch_classify(hipStream_t st, const int8_t* jcomp, const int32_t* j
                            int32_t* ncls, int16_t* jcls) {
     if (nj <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_classify, dim3((nj + 255) / 256), dim3(256), 0, st, jcomp, jcpu, jmem, jgpu, jpart, nj,
-                       static_cast<ClsSlot*>(tab), dem, ncls, jcls);
+                       static_cast<ClsSlot*>(tab), dem, ncls);
+    hipLaunchKernelGGL(k_classify_lookup, dim3((nj + 255) / 256), dim3(256), 0, st, jcomp, jcpu, jmem, jgpu, jpart,
+                       nj, static_cast<const ClsSlot*>(tab), ncls, jcls);
     return hipGetLastError();
 }
 
