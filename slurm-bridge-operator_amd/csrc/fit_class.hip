@@ -302,12 +302,15 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
         __syncthreads();  // B2
         CLS_OPT(o3);
         if (wave == 0) {
-            const unsigned P = S->ctl.pool_n;
+            const unsigned P = (unsigned)__builtin_amdgcn_readfirstlane((int)S->ctl.pool_n);
             uint64_t e[CLS_POOL / 64];
 #pragma unroll
-            for (int j = 0; j < CLS_POOL / 64; ++j) {
-                const unsigned i = lane + 64 * j;
-                e[j] = i < P ? S->pool[i] : KEY_INF;
+            for (int j = 0; j < CLS_POOL / 64; ++j) {  // only the chunks the pool reaches (≈ 32 keys)
+                e[j] = KEY_INF;
+                if ((unsigned)(64 * j) < P) {
+                    const unsigned i = lane + 64 * j;
+                    e[j] = i < P ? S->pool[i] : KEY_INF;
+                }
             }
             uint64_t T = B;  // the new bound
             if (P > (unsigned)CLS_SET) {
@@ -341,6 +344,7 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
             unsigned base = 0;
 #pragma unroll
             for (int j = 0; j < CLS_POOL / 64; ++j) {
+                if ((unsigned)(64 * j) >= P) break;  // uniform
                 const bool in = e[j] < T;
                 const uint64_t bal = __ballot(in);
                 if (in) S->set[cl][base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
