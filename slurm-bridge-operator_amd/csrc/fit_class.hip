@@ -277,6 +277,7 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
         uint64_t k1 = KEY_INF, k2 = KEY_INF;  // this thread's two smallest keys
 #pragma unroll
         for (int i = 0; i < CLS_NPT; ++i) {
+            if (i * CLS_THREADS >= n) break;  // uniform: the rows end
             const int p = tid + CLS_THREADS * i;
             if (p < n) {
                 const uint64_t k = cls_key<false>(rows[p], d.x, d.y, d.z, 0, (uint32_t)p);
@@ -377,6 +378,7 @@ __device__ __forceinline__ unsigned cls_block_op(ClsLds* S, const int4* rows, in
         uint64_t m = KEY_INF;
 #pragma unroll
         for (int i = 0; i < CLS_NPT; ++i) {
+            if (i * CLS_THREADS >= n) break;  // uniform: the rows end
             const int p = tid + CLS_THREADS * i;
             if (p < n) {
                 const uint64_t key = cls_key<true>(rows[p], d.x, d.y, d.z, w, (uint32_t)p);
